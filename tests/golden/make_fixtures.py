@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures under tests/golden/ from the REFERENCE.
+
+Runs only in the build container (needs oracle/_ref, i.e. `make -C oracle`
+with /root/reference present).  The outputs are data (inputs + the
+reference's outputs) and are committed; nothing here ships to the GPU box
+except those files.
+
+  stages_<case>/   stage-level dumps of the reference `--c` path for a small
+                   image (oracle/ref_driver.cc `stages`): reference/candidate
+                   XYB, MHIC planes, edge / block-diff / low-freq / mask /
+                   combined maps, distmap, block weights, per-block zeroing
+                   orders.
+  manifest.json    end-to-end known answers: sha256 / size / iterations of
+                   `guetzli --c` on bees.png and on synthetic frames.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref", "guetzli_ref")
+
+
+def texture_image(w, h, seed):
+    """Smooth colour field + sinusoids + filtered noise (numpy, seeded)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.zeros((h, w, 3))
+    for c in range(3):
+        v = 120.0 + 30.0 * rng.uniform(-1, 1)
+        for _ in range(3):
+            a = rng.uniform(8, 30)
+            fx, fy = rng.uniform(0.02, 0.4, size=2)
+            v = v + a * np.sin(fx * xx + fy * yy + rng.uniform(0, 6.28))
+        noise = rng.normal(0, 10, size=(h, w))
+        k = np.array([1, 4, 6, 4, 1], dtype=np.float64) / 16
+        noise = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 1, noise)
+        img[:, :, c] = v + noise
+    for _ in range(3):
+        x0, y0 = rng.integers(0, w - 8), rng.integers(0, h - 8)
+        x1, y1 = x0 + rng.integers(4, max(5, w // 3)), y0 + rng.integers(4, max(5, h // 3))
+        img[y0:y1, x0:x1, :] = 0.5 * img[y0:y1, x0:x1, :] + 0.5 * rng.uniform(40, 220, size=3)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def flat_image(w, h, seed):
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(60, 200, size=3)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = base[None, None, :] + 0.05 * xx[:, :, None] + 0.03 * yy[:, :, None]
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def bees_crop(x0, y0, w, h):
+    bees = np.fromfile(os.path.join(HERE, "bees.rgb"), dtype=np.uint8).reshape(258, 444, 3)
+    return np.ascontiguousarray(bees[y0:y0 + h, x0:x0 + w])
+
+
+STAGE_CASES = [
+    # name, image factory, qseed
+    ("tex_64x48", lambda: texture_image(64, 48, 1), 1),
+    ("tex_100x77", lambda: texture_image(100, 77, 2), 2),
+    ("tex_41x33", lambda: texture_image(41, 33, 3), 3),
+    ("bees_88x64", lambda: bees_crop(200, 100, 88, 64), 4),
+    ("flat_48x40", lambda: flat_image(48, 40, 5), 5),
+]
+
+
+def sha256(path):
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
+def run_stages():
+    for name, make, qseed in STAGE_CASES:
+        img = make()
+        h, w, _ = img.shape
+        d = os.path.join(HERE, "stages_" + name)
+        os.makedirs(d, exist_ok=True)
+        rgb = os.path.join(d, "input.rgb")
+        img.tofile(rgb)
+        subprocess.run([REF, "stages", rgb, str(w), str(h), str(qseed), d], check=True)
+        print("stages", name, w, h)
+
+
+def run_e2e(manifest, cases):
+    out = manifest.setdefault("e2e", {})
+    for name, rgb, w, h, q in cases:
+        jpg = "/tmp/gz_fixture_%s.jpg" % name
+        res = subprocess.run([REF, "encode", rgb, str(w), str(h), str(q), jpg, "c"], check=True,
+                             capture_output=True, text=True)
+        info = json.loads(res.stdout)
+        out[name] = {"w": w, "h": h, "quality": q, "sha256": sha256(jpg), "bytes": info["bytes"],
+                     "iters": info["iters"], "ref_seconds": info["seconds"],
+                     "input": os.path.relpath(rgb, HERE) if rgb.startswith(HERE) else rgb}
+        print("e2e", name, out[name])
+
+
+def main():
+    manifest_path = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(manifest_path)) if os.path.exists(manifest_path) else {}
+    what = sys.argv[1:] or ["stages", "e2e-small"]
+    if "stages" in what:
+        run_stages()
+    if "e2e-small" in what:
+        cases = [("bees_q95", os.path.join(HERE, "bees.rgb"), 444, 258, 95)]
+        for name, _, _ in STAGE_CASES:
+            d = os.path.join(HERE, "stages_" + name)
+            meta = dict(l.split() for l in open(os.path.join(d, "meta.txt")) if len(l.split()) == 2)
+            cases.append(("%s_q95" % name, os.path.join(d, "input.rgb"), int(meta["w"]),
+                          int(meta["h"]), 95))
+        cases.append(("bees_q90", os.path.join(HERE, "bees.rgb"), 444, 258, 90))
+        cases.append(("bees_q84", os.path.join(HERE, "bees.rgb"), 444, 258, 84))
+        run_e2e(manifest, cases)
+    json.dump(manifest, open(manifest_path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
