@@ -1,0 +1,219 @@
+// extern "C" boundary of libguetzli_hip (include/guetzli_hip.h).
+#include "guetzli_hip.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "host/jpeg_encode.h"
+#include "host/processor.h"
+#include "host/synthetic.h"
+#include "runtime/engine.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gz_status SetError(gz_status st, const std::string& msg) {
+  g_last_error = msg;
+  return st;
+}
+
+}  // namespace
+
+struct gz_comparator {
+  std::unique_ptr<gz::Engine> engine;
+  float target = 0.0f;
+  float distance = 0.0f;
+  int w = 0, h = 0;
+  std::vector<float> block_max;
+};
+
+extern "C" {
+
+const char* gz_last_error(void) { return g_last_error.c_str(); }
+
+const char* gz_build_info(void) { return gz::BuildInfo(); }
+
+int gz_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void gz_params_init(gz_params* p) {
+  if (!p) return;
+  p->butteraugli_target = 1.0f;
+  p->clear_metadata = 1;
+  p->try_420 = 0;
+  p->force_420 = 0;
+  p->use_silver_screen = 0;
+  p->zeroing_greedy_lookahead = 3;
+  p->new_zeroing_model = 1;
+}
+
+double gz_butteraugli_score_for_quality(double quality) {
+  return gz::ButteraugliScoreForQuality(quality);
+}
+
+void gz_free(void* p) { std::free(p); }
+
+gz_status gz_comparator_create(int device, int width, int height, const uint8_t* rgb,
+                               float target_distance, gz_comparator** out) {
+  if (!out || !rgb || width < 8 || height < 8)
+    return SetError(GZ_ERR_INVALID_ARG, "gz_comparator_create: bad argument");
+  std::string err;
+  auto eng = gz::Engine::Create(device, width, height, &err);
+  if (!eng) return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + err);
+  if (!eng->SetReference(rgb, false))
+    return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + eng->error());
+  auto* c = new gz_comparator;
+  c->engine = std::move(eng);
+  c->target = target_distance;
+  c->w = width;
+  c->h = height;
+  *out = c;
+  return GZ_OK;
+}
+
+void gz_comparator_destroy(gz_comparator* cmp) { delete cmp; }
+
+static gz_status CompareImpl(gz_comparator* cmp, const int16_t* coeffs, gz::CompareDebug* dbg,
+                             float* distance) {
+  if (!cmp || !coeffs) return SetError(GZ_ERR_INVALID_ARG, "compare: bad argument");
+  gz::Engine& e = *cmp->engine;
+  cmp->block_max.resize(e.blocks());
+  if (!e.UploadCoeffs(coeffs) || !e.Compare(&cmp->distance, cmp->block_max.data(), dbg))
+    return SetError(GZ_ERR_DEVICE, "compare: " + e.error());
+  if (distance) *distance = cmp->distance;
+  return GZ_OK;
+}
+
+gz_status gz_comparator_compare(gz_comparator* cmp, const int16_t* coeffs, float* distance) {
+  return CompareImpl(cmp, coeffs, nullptr, distance);
+}
+
+gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs,
+                                       gz_compare_stages* st, float* distance) {
+  gz::CompareDebug dbg;
+  if (st) {
+    dbg.cand_linear = st->cand_linear;
+    dbg.cand_xyb = st->cand_xyb;
+    dbg.mhic0 = st->mhic0;
+    dbg.mhic1 = st->mhic1;
+    dbg.edge = st->edge;
+    dbg.block_dc = st->block_dc;
+    dbg.block_ac = st->block_ac;
+    dbg.block_ac_lf = st->block_ac_lf;
+    dbg.mask = st->mask;
+    dbg.mask_dc = st->mask_dc;
+    dbg.combined = st->combined;
+    dbg.distmap = st->distmap;
+  }
+  return CompareImpl(cmp, coeffs, &dbg, distance);
+}
+
+gz_status gz_comparator_block_max(gz_comparator* cmp, float* out) {
+  if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "block_max: bad argument");
+  if (cmp->block_max.empty()) return SetError(GZ_ERR_INVALID_ARG, "block_max: no compare yet");
+  std::memcpy(out, cmp->block_max.data(), cmp->block_max.size() * sizeof(float));
+  return GZ_OK;
+}
+
+int gz_comparator_distance_ok(gz_comparator* cmp, double target_mul) {
+  // butteraugli_comparator.h:52-54
+  return cmp && cmp->distance <= target_mul * cmp->target;
+}
+
+double gz_comparator_score_output_size(gz_comparator* cmp, int size) {
+  return cmp ? gz::ScoreJPEG(cmp->distance, size, cmp->target) : 0.0;
+}
+
+gz_status gz_comparator_start_block_comparisons(gz_comparator* cmp, float* mask_scale) {
+  if (!cmp) return SetError(GZ_ERR_INVALID_ARG, "start_block_comparisons: bad argument");
+  if (!cmp->engine->StartBlockComparisons(mask_scale))
+    return SetError(GZ_ERR_DEVICE, "start_block_comparisons: " + cmp->engine->error());
+  return GZ_OK;
+}
+
+gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* cur_coeffs,
+                                             const int16_t* orig_coeffs, int comp_mask,
+                                             float limit, int lookahead, gz_coeff_data* out) {
+  if (!cmp || !cur_coeffs || !orig_coeffs || !out || lookahead < 1 || comp_mask <= 0 ||
+      comp_mask > 7)
+    return SetError(GZ_ERR_INVALID_ARG, "block_zeroing_orders: bad argument");
+  gz::Engine& e = *cmp->engine;
+  static_assert(sizeof(gz_coeff_data) == sizeof(gz::CoeffDataHost), "CoeffData layout");
+  if (!e.SetOriginalCoeffs(orig_coeffs, false) || !e.UploadCoeffs(cur_coeffs) ||
+      !e.BlockZeroingOrders(comp_mask, limit, lookahead,
+                            reinterpret_cast<gz::CoeffDataHost*>(out)))
+    return SetError(GZ_ERR_DEVICE, "block_zeroing_orders: " + e.error());
+  return GZ_OK;
+}
+
+gz_status gz_synthetic_frame(uint64_t seed, int width, int height, uint8_t* rgb_out) {
+  if (!rgb_out || width <= 0 || height <= 0)
+    return SetError(GZ_ERR_INVALID_ARG, "synthetic_frame: bad argument");
+  gz::SyntheticFrame(seed, width, height, rgb_out);
+  return GZ_OK;
+}
+
+gz_status gz_rgb_to_coeffs(const uint8_t* rgb, int width, int height, int16_t* coeffs_out) {
+  if (!rgb || !coeffs_out || width <= 0 || height <= 0 || width >= (1 << 16) ||
+      height >= (1 << 16))
+    return SetError(GZ_ERR_INVALID_ARG, "rgb_to_coeffs: bad argument");
+  gz::RgbToCoeffsQ1(rgb, width, height, coeffs_out);
+  return GZ_OK;
+}
+
+static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t* rgb,
+                             bool device_ptr, int w, int h, uint8_t** jpeg_out,
+                             size_t* jpeg_size, gz_process_stats* stats) {
+  if (!params || !rgb || !jpeg_out || !jpeg_size || w <= 0 || h <= 0)
+    return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
+  if (params->try_420 || params->force_420)
+    return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output is not supported");
+  gz::ProcessParams pp;
+  pp.butteraugli_target = params->butteraugli_target;
+  pp.clear_metadata = params->clear_metadata != 0;
+  pp.zeroing_greedy_lookahead = params->zeroing_greedy_lookahead;
+  pp.new_zeroing_model = params->new_zeroing_model != 0;
+  gz::ProcessResult res;
+  std::string err;
+  const int rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
+  if (rc != 0) return SetError(rc, "process: " + err);
+  uint8_t* buf = static_cast<uint8_t*>(std::malloc(res.jpeg.size() ? res.jpeg.size() : 1));
+  if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "process: out of host memory");
+  std::memcpy(buf, res.jpeg.data(), res.jpeg.size());
+  *jpeg_out = buf;
+  *jpeg_size = res.jpeg.size();
+  if (stats) {
+    stats->iterations = res.iterations;
+    stats->iterations_up = res.iterations_up;
+    stats->iterations_down = res.iterations_down;
+    stats->compares = res.compares;
+    stats->seconds_compare = res.seconds_compare;
+    stats->seconds_zeroing = res.seconds_zeroing;
+    stats->seconds_total = res.seconds_total;
+  }
+  return GZ_OK;
+}
+
+gz_status gz_process_rgb(int device, const gz_params* params, const uint8_t* rgb, int width,
+                         int height, uint8_t** jpeg_out, size_t* jpeg_size,
+                         gz_process_stats* stats) {
+  return ProcessImpl(device, params, rgb, false, width, height, jpeg_out, jpeg_size, stats);
+}
+
+gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8_t* rgb_dev,
+                                int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
+                                gz_process_stats* stats) {
+  return ProcessImpl(device, params, rgb_dev, true, width, height, jpeg_out, jpeg_size, stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// Host-side JPEG container model of the search loop (the subset of
+// guetzli::JPEGData, guetzli/jpeg_data.h:138-204, that a 4:4:4 baseline
+// Huffman encode needs) and the coefficient image the loop edits
+// (guetzli::OutputImage restricted to factor-1 components,
+// guetzli/output_image.h).
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace gz {
+
+using coeff_t = int16_t;
+constexpr int kDCTBlockSize = 64;
+
+extern const int kJPEGNaturalOrder[64];  // zigzag position -> natural index
+extern const int kJPEGZigZagOrder[64];   // natural index -> zigzag position
+
+struct QuantTable {
+  int values[kDCTBlockSize];
+  int precision = 0;
+  int index = 0;
+};
+
+struct JpegComponent {
+  int id = 0;
+  int h_samp_factor = 1;
+  int v_samp_factor = 1;
+  int quant_idx = 0;
+  int width_in_blocks = 0;
+  int height_in_blocks = 0;
+  std::vector<coeff_t> coeffs;  // [blocks][64], natural order
+};
+
+struct JpegData {
+  int width = 0;
+  int height = 0;
+  int max_h_samp_factor = 1;
+  int max_v_samp_factor = 1;
+  int mcu_rows = 0;
+  int mcu_cols = 0;
+  std::vector<std::string> app_data;
+  std::vector<std::string> com_data;
+  std::vector<QuantTable> quant;
+  std::vector<JpegComponent> components;
+};
+
+// InitJPEGDataForYUV444 + AddApp0Data (jpeg_data.cc:49-69,
+// jpeg_data_encoder.cc:51-63).
+void InitJpegDataYUV444(int w, int h, JpegData* jpg);
+// SaveQuantTables (jpeg_data.cc:71-101): de-duplicates identical tables.
+void SaveQuantTables(const int q[3][kDCTBlockSize], JpegData* jpg);
+
+// Coefficient image (4:4:4).  coeffs is [3][blocks][64] of DEQUANTISED
+// values (quantized value * quant), as OutputImageComponent stores them.
+struct CoeffImage {
+  int width = 0, height = 0, block_w = 0, block_h = 0, blocks = 0;
+  std::vector<coeff_t> coeffs;
+  int quant[3][kDCTBlockSize];
+  // Bumped on every host-side change so a device mirror knows when to re-upload.
+  uint64_t version = 0;
+
+  void Init(int w, int h);
+  coeff_t* block(int c, int block_ix) { return &coeffs[(static_cast<size_t>(c) * blocks + block_ix) * 64]; }
+  const coeff_t* block(int c, int block_ix) const {
+    return &coeffs[(static_cast<size_t>(c) * blocks + block_ix) * 64];
+  }
+  // CopyFromJpegData (output_image.cc:481-492, 212-228)
+  void CopyFromJpegData(const JpegData& jpg);
+  // ApplyGlobalQuantization on the host (output_image.cc:349-360, 573-577)
+  void ApplyGlobalQuantization(const int q[3][kDCTBlockSize]);
+  // SaveToJpegData (output_image.cc:579-640)
+  void SaveToJpegData(JpegData* jpg) const;
+  bool ComponentIsAllZero(int c) const;
+};
+
+// Quantize (guetzli/quantize.h:25-30)
+inline coeff_t QuantizeCoeff(coeff_t raw, int quant) {
+  const int r = raw % quant;
+  const coeff_t delta = 2 * r > quant ? quant - r : (-2) * r > quant ? -quant - r : -r;
+  return static_cast<coeff_t>(raw + delta);
+}
+
+}  // namespace gz

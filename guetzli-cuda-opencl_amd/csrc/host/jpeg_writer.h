@@ -1,0 +1,42 @@
+// Baseline Huffman JPEG serializer and the entropy-size estimator used by the
+// search loop (guetzli/jpeg_data_writer.cc, entropy_encode.cc,
+// jpeg_bit_writer.h).  Output bytes are identical to the reference writer.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "host/jpeg_model.h"
+
+namespace gz {
+
+// Symbol histogram; every symbol is counted twice and a fake symbol 256 with
+// count 1 guarantees it gets the all-ones code (jpeg_data_writer.h:63-92).
+struct JpegHistogram {
+  static const int kSize = 257;
+  uint32_t counts[kSize];
+  JpegHistogram() { Clear(); }
+  void Clear();
+  void Add(int symbol) { counts[symbol] += 2; }
+  void Add(int symbol, int weight) { counts[symbol] += 2 * weight; }
+  void AddHistogram(const JpegHistogram& other);
+  int NumSymbols() const;
+};
+
+// Length-limited Huffman code lengths (CreateHuffmanTree, entropy_encode.cc:65-145).
+void HuffmanCodeLengths(const uint32_t* counts, int length, int max_depth, uint8_t* depth);
+
+size_t HistogramHeaderCost(const JpegHistogram& h);
+size_t HistogramEntropyCost(const JpegHistogram& h, const uint8_t depths[256]);
+void BuildDCHistograms(const JpegData& jpg, JpegHistogram* histo);
+void BuildACHistograms(const JpegData& jpg, JpegHistogram* histo);
+size_t JpegHeaderSize(const JpegData& jpg, bool strip_metadata);
+size_t ClusterHistograms(JpegHistogram* histo, size_t* num, int* histo_indexes, uint8_t* depths);
+
+// WriteJpeg (jpeg_data_writer.cc:540-553).  Appends to *out.
+bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out);
+
+}  // namespace gz

@@ -1,0 +1,702 @@
+// The Guetzli search loop on the host (guetzli/processor.cc), driving the GPU
+// comparator.  Control flow, heuristics and every floating-point decision are
+// those of the reference's CPU_OPT (`guetzli --c`) path so the output bytes
+// are identical; only the expensive work (Butteraugli passes, per-block
+// greedy zeroing, global quantization) runs on the device.
+#include "host/processor.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <set>
+#include <utility>
+
+#include <hip/hip_runtime.h>
+
+#include "guetzli_hip.h"
+#include "host/jpeg_encode.h"
+#include "host/jpeg_writer.h"
+
+namespace gz {
+
+// ---------------------------------------------------------------------------
+// quality.cc / score.cc
+// ---------------------------------------------------------------------------
+
+double ButteraugliScoreForQuality(double quality) {
+  static const double kScoreForQuality[] = {
+      2.810761, 2.729300, 2.689687, 2.636811, 2.547863, 2.525400, 2.473416, 2.366133, 2.338078,
+      2.318654, 2.201674, 2.145517, 2.087322, 2.009328, 1.945456, 1.900112, 1.805701, 1.750194,
+      1.644175, 1.562165, 1.473608, 1.382021, 1.294298, 1.185402, 1.066781, 0.971769, 0.852901,
+      0.724544, 0.611302, 0.443185, 0.211578, 0.209462, 0.207346, 0.205230, 0.203114, 0.200999,
+      0.198883, 0.196767, 0.194651, 0.192535, 0.190420, 0.190420,
+  };
+  const int kLowest = 70, kHighest = 110;
+  if (quality < kLowest) quality = kLowest;
+  if (quality > kHighest) quality = kHighest;
+  const int index = static_cast<int>(quality);
+  const double mix = quality - index;
+  return kScoreForQuality[index - kLowest] * (1 - mix) + kScoreForQuality[index - kLowest + 1] * mix;
+}
+
+double ScoreJPEG(double distance, int size, double target) {
+  const double kScale = 50, kMaxExponent = 10, kLargeSize = 1e30;
+  const double diff = distance - target;
+  if (diff <= 0.0) return size;
+  const double exponent = kScale * diff;
+  if (exponent > kMaxExponent) return kLargeSize * std::exp(kMaxExponent) * diff + size;
+  return std::exp(exponent) * size;
+}
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+inline double Since(Clock::time_point t0) {
+  return std::chrono::duration<double>(Clock::now() - t0).count();
+}
+
+inline int Log2FloorNonZero(uint32_t n) { return 31 ^ __builtin_clz(n); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// HipButteraugliComparator
+// ---------------------------------------------------------------------------
+
+std::unique_ptr<HipButteraugliComparator> HipButteraugliComparator::Create(
+    int device, int w, int h, const uint8_t* rgb, bool device_ptr, float target, std::string* err) {
+  std::unique_ptr<HipButteraugliComparator> c(new HipButteraugliComparator);
+  c->engine_ = Engine::Create(device, w, h, err);
+  if (!c->engine_) return nullptr;
+  if (!c->engine_->SetReference(rgb, device_ptr)) {
+    if (err) *err = c->engine_->error();
+    return nullptr;
+  }
+  c->w_ = w;
+  c->h_ = h;
+  c->target_ = target;
+  c->block_max_.assign(c->engine_->blocks(), 0.0f);
+  return c;
+}
+
+bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
+  std::vector<coeff_t> all;
+  for (int c = 0; c < 3; ++c)
+    all.insert(all.end(), jpg.components[c].coeffs.begin(), jpg.components[c].coeffs.end());
+  if (!engine_->SetOriginalCoeffs(all.data(), false)) {
+    err_ = engine_->error();
+    return false;
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::Compare(const CoeffImage& img) {
+  const auto t0 = Clock::now();
+  if (device_version_ != img.version) {
+    if (!engine_->UploadCoeffs(img.coeffs.data())) {
+      err_ = engine_->error();
+      return false;
+    }
+    device_version_ = img.version;
+  }
+  if (!engine_->Compare(&distance_, block_max_.data(), nullptr)) {
+    err_ = engine_->error();
+    return false;
+  }
+  ++compares;
+  seconds_compare += Since(t0);
+  return true;
+}
+
+bool HipButteraugliComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) {
+  if (!engine_->QuantizeFromOriginal(q, img->coeffs.data())) {
+    err_ = engine_->error();
+    return false;
+  }
+  for (int c = 0; c < 3; ++c) std::memcpy(img->quant[c], q[c], sizeof(img->quant[c]));
+  ++img->version;
+  device_version_ = img->version;
+  return true;
+}
+
+bool HipButteraugliComparator::StartBlockComparisons() {
+  if (!engine_->StartBlockComparisons(nullptr)) {
+    err_ = engine_->error();
+    return false;
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::BlockZeroingOrders(const CoeffImage& img, const JpegData&,
+                                                  int comp_mask, int lookahead,
+                                                  std::vector<CoeffData>* out) {
+  const auto t0 = Clock::now();
+  if (device_version_ != img.version) {
+    if (!engine_->UploadCoeffs(img.coeffs.data())) {
+      err_ = engine_->error();
+      return false;
+    }
+    device_version_ = img.version;
+  }
+  out->resize(static_cast<size_t>(img.blocks) * 192);
+  static_assert(sizeof(CoeffData) == sizeof(CoeffDataHost), "CoeffData layout");
+  if (!engine_->BlockZeroingOrders(comp_mask, target_, lookahead,
+                                   reinterpret_cast<CoeffDataHost*>(out->data()))) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_zeroing += Since(t0);
+  return true;
+}
+
+double HipButteraugliComparator::ScoreOutputSize(int size) const {
+  return ScoreJPEG(distance_, size, target_);
+}
+
+void HipButteraugliComparator::ComputeBlockErrorAdjustmentWeights(
+    int direction, int max_block_dist, double target_mul, int factor_x, int factor_y,
+    const std::vector<float>& max_dist_per_block, std::vector<float>* block_weight) {
+  BlockErrorAdjustmentWeights(w_, h_, target_, direction, max_block_dist, target_mul, factor_x,
+                              factor_y, max_dist_per_block, block_weight);
+}
+
+void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int max_block_dist,
+                                 double target_mul, int factor_x, int factor_y,
+                                 const std::vector<float>& max_dist_per_block,
+                                 std::vector<float>* block_weight) {
+  // butteraugli_comparator.cc:169-233 (block maxima come from the device)
+  const double target_distance = target * target_mul;
+  const int sizex = 8 * factor_x, sizey = 8 * factor_y;
+  const int bw = (w + sizex - 1) / sizex, bh = (h + sizey - 1) / sizey;
+  for (int by = 0; by < bh; ++by) {
+    for (int bx = 0; bx < bw; ++bx) {
+      const int bix = by * bw + bx;
+      float max_local = static_cast<float>(target_distance);
+      const int x0 = std::max(0, bx - max_block_dist), y0 = std::max(0, by - max_block_dist);
+      const int x1 = std::min(bw, bx + 1 + max_block_dist), y1 = std::min(bh, by + 1 + max_block_dist);
+      for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) max_local = std::max(max_local, max_dist_per_block[y * bw + x]);
+      if (direction > 0) {
+        if (max_dist_per_block[bix] <= target_distance && max_local <= 1.1 * target_distance)
+          (*block_weight)[bix] = 1.0;
+      } else {
+        constexpr double kLocalMaxWeight = 0.5;
+        if (max_dist_per_block[bix] <=
+            (1 - kLocalMaxWeight) * target_distance + kLocalMaxWeight * max_local)
+          continue;
+        for (int y = y0; y < y1; ++y)
+          for (int x = x0; x < x1; ++x) {
+            const int d = std::max(std::abs(y - by), std::abs(x - bx));
+            const int ix = y * bw + x;
+            (*block_weight)[ix] = std::max<float>((*block_weight)[ix], 1.0f / (d + 1.0f));
+          }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Processor
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct QuantData {
+  int q[3][kDCTBlockSize];
+  size_t jpg_size;
+  bool dist_ok;
+};
+
+double ContrastSensitivity(int k) { return 1.0 / (1.0 + kJPEGZigZagOrder[k] / 2.0); }
+
+double QuantMatrixHeuristicScore(const int q[3][kDCTBlockSize]) {
+  double score = 0.0;
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < kDCTBlockSize; ++k) score += 0.5 * (q[c][k] - 1.0) * ContrastSensitivity(k);
+  return score;
+}
+
+// -1 / 0 / 1 / 2 ordering of two quant matrices (processor.cc:168-190).
+int CompareQuantMatrices(const int* a, const int* b) {
+  const int n = 3 * kDCTBlockSize;
+  int i = 0;
+  while (i < n && a[i] == b[i]) ++i;
+  if (i == n) return 0;
+  if (a[i] < b[i]) {
+    for (++i; i < n; ++i)
+      if (a[i] > b[i]) return 2;
+    return -1;
+  }
+  for (++i; i < n; ++i)
+    if (a[i] < b[i]) return 2;
+  return 1;
+}
+
+bool CompareQuantData(const QuantData& a, const QuantData& b) {
+  if (a.dist_ok && !b.dist_ok) return true;
+  if (!a.dist_ok && b.dist_ok) return false;
+  return a.jpg_size < b.jpg_size;
+}
+
+// Binary search over the heuristic quantization "score" (processor.cc:206-308).
+class QuantMatrixGenerator {
+ public:
+  QuantMatrixGenerator() {
+    for (int k = 0; k < kDCTBlockSize; ++k) total_csf_ += 3.0 * ContrastSensitivity(k);
+  }
+  bool GetNext(int q[3][kDCTBlockSize]) {
+    for (int iter = 0; iter < 1000; iter++) {
+      double hscore;
+      if (hscore_b_ == -1.0) {
+        if (hscore_a_ == -1.0) {
+          hscore = total_csf_;
+        } else if (hscore_a_ < 5.0 * total_csf_) {
+          hscore = hscore_a_ + total_csf_;
+        } else {
+          hscore = 2 * (hscore_a_ + total_csf_);
+        }
+        if (hscore > 100 * total_csf_) return false;
+      } else if (hscore_b_ == 0.0) {
+        return false;
+      } else if (hscore_a_ == -1.0) {
+        hscore = 0.0;
+      } else {
+        int lower_q[3][kDCTBlockSize], upper_q[3][kDCTBlockSize];
+        constexpr double kEps = 0.05;
+        MatrixForScore((1 - kEps) * hscore_a_ + kEps * 0.5 * (hscore_a_ + hscore_b_), lower_q);
+        MatrixForScore((1 - kEps) * hscore_b_ + kEps * 0.5 * (hscore_a_ + hscore_b_), upper_q);
+        if (CompareQuantMatrices(&lower_q[0][0], &upper_q[0][0]) == 0) return false;
+        hscore = (hscore_a_ + hscore_b_) * 0.5;
+      }
+      MatrixForScore(hscore, q);
+      bool retry = false;
+      for (const QuantData& d : quants_) {
+        if (CompareQuantMatrices(&q[0][0], &d.q[0][0]) == 0) {
+          if (d.dist_ok) hscore_a_ = hscore; else hscore_b_ = hscore;
+          retry = true;
+          break;
+        }
+      }
+      if (!retry) return true;
+    }
+    return false;
+  }
+  void Add(const QuantData& d) {
+    quants_.push_back(d);
+    const double hscore = QuantMatrixHeuristicScore(d.q);
+    if (d.dist_ok) hscore_a_ = std::max(hscore_a_, hscore);
+    else hscore_b_ = hscore_b_ == -1.0 ? hscore : std::min(hscore_b_, hscore);
+  }
+
+ private:
+  void MatrixForScore(double score, int q[3][kDCTBlockSize]) const {
+    const int level = static_cast<int>(score / total_csf_);
+    score -= level * total_csf_;
+    for (int k = kDCTBlockSize - 1; k >= 0; --k) {
+      for (int c = 0; c < 3; ++c) q[c][kJPEGNaturalOrder[k]] = 2 * level + (score > 0.0 ? 3 : 1);
+      score -= 3.0 * ContrastSensitivity(kJPEGNaturalOrder[k]);
+    }
+  }
+  double hscore_a_ = -1.0, hscore_b_ = -1.0, total_csf_ = 0.0;
+  std::vector<QuantData> quants_;
+};
+
+void UpdateACHistogram(int weight, const coeff_t* coeffs, const int* q, JpegHistogram* h) {
+  // processor.cc:491-515
+  int r = 0;
+  for (int k = 1; k < 64; ++k) {
+    const int kn = kJPEGNaturalOrder[k];
+    const coeff_t c = coeffs[kn];
+    if (c == 0) {
+      ++r;
+      continue;
+    }
+    while (r > 15) {
+      h->Add(0xf0, weight);
+      r -= 16;
+    }
+    h->Add((r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1, weight);
+    r = 0;
+  }
+  if (r > 0) h->Add(0, weight);
+}
+
+size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::vector<uint8_t>* depths) {
+  // processor.cc:517-536
+  std::vector<JpegHistogram> clustered = histograms;
+  size_t num = histograms.size();
+  std::vector<int> indexes(num);
+  std::vector<uint8_t> cdepths(num * JpegHistogram::kSize);
+  ClusterHistograms(clustered.data(), &num, indexes.data(), cdepths.data());
+  depths->resize(cdepths.size());
+  for (size_t i = 0; i < histograms.size(); ++i)
+    std::memcpy(&(*depths)[i * JpegHistogram::kSize], &cdepths[indexes[i] * JpegHistogram::kSize],
+                JpegHistogram::kSize);
+  size_t size = 0;
+  for (size_t i = 0; i < num; ++i) size += HistogramHeaderCost(clustered[i]) / 8;
+  return size;
+}
+
+size_t EntropyCodedDataSize(const std::vector<JpegHistogram>& histograms,
+                            const std::vector<uint8_t>& depths) {
+  size_t bits = 0;
+  for (size_t i = 0; i < histograms.size(); ++i)
+    bits += HistogramEntropyCost(histograms[i], &depths[i * JpegHistogram::kSize]);
+  return (bits + 7) / 8;
+}
+
+size_t EstimateDCSize(const JpegData& jpg) {
+  std::vector<JpegHistogram> h(jpg.components.size());
+  BuildDCHistograms(jpg, h.data());
+  size_t num = h.size();
+  std::vector<int> idx(num);
+  std::vector<uint8_t> depths(num * JpegHistogram::kSize);
+  return ClusterHistograms(h.data(), &num, idx.data(), depths.data());
+}
+
+class Processor {
+ public:
+  Processor(const ProcessParams& p, Comparator* cmp, ProcessResult* res)
+      : params_(p), cmp_(cmp), res_(res) {}
+  int Run(const JpegData& jpg_in, std::string* err);
+
+ private:
+  bool Fail(std::string* err) {
+    if (err) *err = cmp_->error();
+    return false;
+  }
+  void OutputJpeg(const JpegData& jpg, std::string* out) {
+    out->clear();
+    WriteJpeg(jpg, params_.clear_metadata, out);
+  }
+  void MaybeOutput(const std::string& encoded) {
+    const double score = cmp_->ScoreOutputSize(static_cast<int>(encoded.size()));
+    if (score < final_score_ || final_score_ < 0) {
+      res_->jpeg = encoded;
+      final_score_ = score;
+    }
+  }
+  bool TryQuantMatrix(const JpegData& jpg_in, float target_mul, const int q[3][kDCTBlockSize],
+                      CoeffImage* img, QuantData* data, std::string* err);
+  bool SelectQuantMatrix(const JpegData& jpg_in, int best_q[3][kDCTBlockSize], CoeffImage* img,
+                         bool* ok, std::string* err);
+  bool SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int comp_mask,
+                              double target_mul, bool stop_early, std::string* err);
+  bool SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int comp_mask,
+                              double target_mul, bool stop_early,
+                              const std::vector<int>& offsets, const std::vector<uint8_t>& coeffs,
+                              const std::vector<float>& errors, std::string* err);
+
+  ProcessParams params_;
+  Comparator* cmp_;
+  ProcessResult* res_;
+  double final_score_ = -1;
+};
+
+bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
+                               const int q[3][kDCTBlockSize], CoeffImage* img, QuantData* data,
+                               std::string* err) {
+  // processor.cc:310-338
+  std::memcpy(data->q, q, sizeof(data->q));
+  if (!cmp_->QuantizeFromOriginal(q, img)) return Fail(err);
+  std::string encoded;
+  {
+    JpegData out = jpg_in;
+    img->SaveToJpegData(&out);
+    OutputJpeg(out, &encoded);
+  }
+  ++res_->iterations;
+  if (!cmp_->Compare(*img)) return Fail(err);
+  data->dist_ok = cmp_->DistanceOK(target_mul);
+  data->jpg_size = encoded.size();
+  MaybeOutput(encoded);
+  return true;
+}
+
+bool Processor::SelectQuantMatrix(const JpegData& jpg_in, int best_q[3][kDCTBlockSize],
+                                  CoeffImage* img, bool* ok, std::string* err) {
+  // processor.cc:340-372
+  QuantMatrixGenerator qgen;
+  const float target_mul_high = 0.97f, target_mul_low = 0.95f;
+  QuantData best;
+  if (!TryQuantMatrix(jpg_in, target_mul_high, best_q, img, &best, err)) return false;
+  for (;;) {
+    int q_next[3][kDCTBlockSize];
+    if (!qgen.GetNext(q_next)) break;
+    QuantData data;
+    if (!TryQuantMatrix(jpg_in, target_mul_high, q_next, img, &data, err)) return false;
+    qgen.Add(data);
+    if (CompareQuantData(data, best)) {
+      best = data;
+      if (data.dist_ok && !cmp_->DistanceOK(target_mul_low)) break;
+    }
+  }
+  std::memcpy(best_q, best.q, sizeof(best.q));
+  *ok = best.dist_ok;
+  return true;
+}
+
+bool Processor::SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int comp_mask,
+                                       double target_mul, bool stop_early, std::string* err) {
+  // processor.cc:559-721 (the CPU_OPT loop runs as one batched device call)
+  const int num_blocks = img->blocks;
+  if (!cmp_->StartBlockComparisons()) return Fail(err);
+  std::vector<CoeffData> order;
+  if (!cmp_->BlockZeroingOrders(*img, jpg, comp_mask, params_.zeroing_greedy_lookahead, &order))
+    return Fail(err);
+  std::vector<int> offsets(num_blocks + 1);
+  std::vector<uint8_t> cand;
+  std::vector<float> cand_err;
+  const float limit = cmp_->BlockErrorLimit();
+  for (int b = 0; b < num_blocks; ++b) {
+    const CoeffData* p = &order[static_cast<size_t>(b) * 192];
+    offsets[b] = static_cast<int>(cand.size());
+    for (int i = 0; i < 192; ++i) {
+      if (p[i].block_err > 0 && p[i].block_err <= limit) {
+        cand.push_back(static_cast<uint8_t>(p[i].idx));
+        cand_err.push_back(p[i].block_err);
+      }
+    }
+  }
+  cmp_->FinishBlockComparisons();
+  offsets[num_blocks] = static_cast<int>(cand.size());
+  return SelectFrequencyBackEnd(jpg, img, comp_mask, target_mul, stop_early, offsets, cand,
+                                cand_err, err);
+}
+
+bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int comp_mask,
+                                       double target_mul, bool stop_early,
+                                       const std::vector<int>& offsets,
+                                       const std::vector<uint8_t>& cand,
+                                       const std::vector<float>& cand_err, std::string* err) {
+  // processor.cc:723-919
+  const int ncomp = static_cast<int>(jpg.components.size());
+  const int block_width = img->block_w, block_height = img->block_h;
+  const int num_blocks = block_width * block_height;
+  (void)comp_mask;
+  (void)block_height;
+  std::vector<JpegHistogram> ac_histograms(ncomp);
+  int jpg_header_size, dc_size;
+  {
+    JpegData out = jpg;
+    img->SaveToJpegData(&out);
+    jpg_header_size = static_cast<int>(JpegHeaderSize(out, params_.clear_metadata));
+    dc_size = static_cast<int>(EstimateDCSize(out));
+    BuildACHistograms(out, ac_histograms.data());
+  }
+  std::vector<uint8_t> ac_depths;
+  int ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+  const int base_size = jpg_header_size + dc_size + ac_histogram_size +
+                        static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+  int prev_size = base_size;
+  std::vector<float> max_block_error(num_blocks, 0.0f);
+  std::vector<int> last_indexes(num_blocks, 0);
+  const std::vector<float> zero_block_max(num_blocks, 0.0f);
+  bool first_up_iter = true;
+  for (int direction : {1, -1}) {
+    for (;;) {
+      if (stop_early && direction == -1 && prev_size > 1.01 * res_->jpeg.size()) break;
+      std::vector<std::pair<int, float>> global_order;
+      int blocks_to_change = 0;
+      std::vector<float> block_weight;
+      for (int rblock = 1; rblock <= 4; ++rblock) {
+        block_weight.assign(num_blocks, 0.0f);
+        const std::vector<float>& bmax = first_up_iter ? zero_block_max : cmp_->block_max_distance();
+        cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, 1, 1, bmax,
+                                                 &block_weight);
+        global_order.clear();
+        blocks_to_change = 0;
+        for (int bix = 0; bix < num_blocks; ++bix) {
+          const int last_index = last_indexes[bix];
+          const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
+          const int num_candidates = offsets[bix + 1] - offset;
+          const float* errs = cand_err.data() + offset;
+          const float max_err = max_block_error[bix];
+          if (block_weight[bix] == 0) continue;
+          if (direction > 0) {
+            for (size_t i = last_index; i < static_cast<size_t>(num_candidates); ++i)
+              global_order.push_back(std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]));
+            blocks_to_change += last_index < num_candidates ? 1 : 0;
+          } else {
+            for (int i = last_index - 1; i >= 0; --i)
+              global_order.push_back(std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]));
+            blocks_to_change += last_index > 0 ? 1 : 0;
+          }
+        }
+        if (!global_order.empty()) break;
+      }
+      if (global_order.empty()) break;
+      std::sort(global_order.begin(), global_order.end(),
+                [](const std::pair<int, float>& a, const std::pair<int, float>& b) {
+                  return a.second < b.second;
+                });
+      double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
+      if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
+      const double min_size_delta = base_size * rel_size_delta;
+      const float per_block = direction > 0 ? 2.0f : 1 * 1 * 0.2f;
+      int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
+      if (first_up_iter) {
+        const float limit = 0.75f * cmp_->BlockErrorLimit();
+        auto it = std::partition_point(global_order.begin(), global_order.end(),
+                                       [=](const std::pair<int, float>& a) { return a.second < limit; });
+        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, static_cast<int>(it - global_order.begin()));
+        first_up_iter = false;
+      }
+      float val_threshold = 0.0f;
+      int changed_coeffs = 0;
+      int est_jpg_size = prev_size;
+      for (size_t i = 0; i < global_order.size(); ++i) {
+        const int bix = global_order[i].first;
+        const int bx = bix % block_width, by = bix / block_width;
+        const int last_idx = last_indexes[bix];
+        const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+        const int idx = cand[offset + last_idx + std::min(direction, 0)];
+        const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+        const int* quant = img->quant[c];
+        const JpegComponent& comp = jpg.components[c];
+        const int jpg_bix = by * comp.width_in_blocks + bx;
+        const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
+        coeff_t* block = img->block(c, bix);
+        UpdateACHistogram(-1, block, quant, &ac_histograms[c]);
+        block[k] = static_cast<coeff_t>(newval);
+        UpdateACHistogram(1, block, quant, &ac_histograms[c]);
+        last_indexes[bix] += direction;
+        val_threshold = global_order[i].second;
+        ++changed_coeffs;
+        if (i % 10 == 0) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+        est_jpg_size = jpg_header_size + dc_size + ac_histogram_size +
+                       static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+        if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta)
+          break;
+      }
+      ++img->version;
+      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
+      ++res_->iterations;
+      if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
+      std::string encoded;
+      {
+        JpegData out = jpg;
+        img->SaveToJpegData(&out);
+        OutputJpeg(out, &encoded);
+      }
+      if (!cmp_->Compare(*img)) return Fail(err);
+      MaybeOutput(encoded);
+      prev_size = est_jpg_size;
+    }
+  }
+  return true;
+}
+
+int Processor::Run(const JpegData& jpg_in, std::string* err) {
+  // ProcessJpegData, processor.cc:931-1020 (4:4:4, no 4:2:0 trial)
+  if (params_.butteraugli_target > 2.0f) {
+    if (err) *err = "butteraugli target above 2.0 (quality below 84) is not supported";
+    return GZ_ERR_INVALID_ARG;
+  }
+  std::string encoded;
+  OutputJpeg(jpg_in, &encoded);
+  final_score_ = -1;
+  if (cmp_ == nullptr) {  // image too small for Butteraugli
+    res_->jpeg = encoded;
+    return GZ_OK;
+  }
+  auto remove_quant = [](JpegData* jpg, int q_in[3][kDCTBlockSize]) {
+    // RemoveOriginalQuantization, processor.cc:94-107
+    for (int i = 0; i < 3; ++i) {
+      JpegComponent& c = jpg->components[i];
+      const int* q = jpg->quant[c.quant_idx].values;
+      std::memcpy(q_in[i], q, sizeof(q_in[i]));
+      for (size_t j = 0; j < c.coeffs.size(); ++j) c.coeffs[j] = static_cast<coeff_t>(c.coeffs[j] * q[j % 64]);
+    }
+    int ones[3][kDCTBlockSize];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < kDCTBlockSize; ++j) ones[i][j] = 1;
+    SaveQuantTables(ones, jpg);
+  };
+  int q_in[3][kDCTBlockSize];
+  JpegData jpg = jpg_in;
+  remove_quant(&jpg, q_in);
+  auto device_error = [&]() {
+    Fail(err);
+    return GZ_ERR_DEVICE;
+  };
+  if (!cmp_->SetOriginalCoeffs(jpg)) return device_error();
+  CoeffImage img;
+  img.Init(jpg.width, jpg.height);
+  img.CopyFromJpegData(jpg);
+  if (!cmp_->Compare(img)) return device_error();
+  MaybeOutput(encoded);
+  img.CopyFromJpegData(jpg);
+  int best_q[3][kDCTBlockSize];
+  std::memcpy(best_q, q_in, sizeof(best_q));
+  bool ok = false;
+  if (!SelectQuantMatrix(jpg, best_q, &img, &ok, err)) return GZ_ERR_DEVICE;
+  if (!ok)
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
+  if (!cmp_->QuantizeFromOriginal(best_q, &img)) return device_error();
+  if (!SelectFrequencyMasking(jpg, &img, 7, 1.0, false, err)) return GZ_ERR_DEVICE;
+  return GZ_OK;
+}
+
+}  // namespace
+
+void EncodeRGBToJpegData(const uint8_t* rgb, int w, int h, JpegData* jpg) {
+  InitJpegDataYUV444(w, h, jpg);
+  for (auto& q : jpg->quant)
+    for (int k = 0; k < kDCTBlockSize; ++k) q.values[k] = 1;
+  const size_t nb = static_cast<size_t>(jpg->mcu_cols) * jpg->mcu_rows;
+  std::vector<coeff_t> all(nb * 64 * 3);
+  RgbToCoeffsQ1(rgb, w, h, all.data());
+  for (int c = 0; c < 3; ++c)
+    std::memcpy(jpg->components[c].coeffs.data(), all.data() + c * nb * 64, nb * 64 * sizeof(coeff_t));
+}
+
+int ProcessJpegData(const ProcessParams& params, const JpegData& jpg, Comparator* cmp,
+                    ProcessResult* result, std::string* err) {
+  Processor proc(params, cmp, result);
+  return proc.Run(jpg, err);
+}
+
+int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool device_ptr, int w,
+            int h, ProcessResult* result, std::string* err) {
+  // guetzli::Process(params, stats, rgb, w, h, out), processor.cc:1157-1185
+  const auto t0 = Clock::now();
+  if (w <= 0 || h <= 0 || w >= (1 << 16) || h >= (1 << 16)) {
+    if (err) *err = "Could not create jpg data from rgb pixels";
+    return GZ_ERR_INVALID_ARG;
+  }
+  std::vector<uint8_t> host_rgb;
+  const uint8_t* hrgb = rgb;
+  if (device_ptr) {
+    host_rgb.resize(static_cast<size_t>(3) * w * h);
+    if (hipSetDevice(device) != hipSuccess ||
+        hipMemcpy(host_rgb.data(), rgb, host_rgb.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+      if (err) *err = "device rgb copy failed";
+      return GZ_ERR_DEVICE;
+    }
+    hrgb = host_rgb.data();
+  }
+  JpegData jpg;
+  EncodeRGBToJpegData(hrgb, w, h, &jpg);
+  std::unique_ptr<HipButteraugliComparator> cmp;
+  if (w >= 32 && h >= 32) {
+    std::string e;
+    cmp = HipButteraugliComparator::Create(device, w, h, rgb, device_ptr, params.butteraugli_target, &e);
+    if (!cmp) {
+      if (err) *err = e;
+      return GZ_ERR_DEVICE;
+    }
+  }
+  const int rc = ProcessJpegData(params, jpg, cmp.get(), result, err);
+  if (cmp) {
+    result->compares = cmp->compares;
+    result->seconds_compare = cmp->seconds_compare;
+    result->seconds_zeroing = cmp->seconds_zeroing;
+  }
+  result->seconds_total = Since(t0);
+  return rc;
+}
+
+}  // namespace gz

@@ -1,0 +1,128 @@
+// Host side of the search: the Processor loop (guetzli/processor.cc) and the
+// Comparator surface it drives (guetzli/comparator.h:29-96), with the
+// Butteraugli comparator implemented on the GPU engine.
+#pragma once
+
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host/jpeg_model.h"
+#include "runtime/engine.h"
+
+namespace gz {
+
+// guetzli/quality.cc:78-87
+double ButteraugliScoreForQuality(double quality);
+// guetzli/score.cc:23-43
+double ScoreJPEG(double butteraugli_distance, int size, double butteraugli_target);
+
+struct CoeffData {  // guetzli::CoeffData, processor.h:29-32
+  int idx;
+  float block_err;
+};
+
+// The comparator interface the search loop talks to.  Mirrors
+// guetzli::Comparator (comparator.h:29-96); the per-block pair
+// SwitchBlock()/CompareBlock() becomes one batched call over all blocks
+// (the shape of the reference GPU fast path, processor.cc:580-634), and
+// distmap() is consumed only through its per-block maxima.
+class Comparator {
+ public:
+  virtual ~Comparator() {}
+  virtual bool Compare(const CoeffImage& img) = 0;
+  virtual bool StartBlockComparisons() = 0;
+  virtual void FinishBlockComparisons() = 0;
+  virtual bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
+                                  int lookahead, std::vector<CoeffData>* out) = 0;
+  // Device-side CopyFromJpegData(q=1) + ApplyGlobalQuantization(q); fills img.
+  virtual bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) = 0;
+  virtual double ScoreOutputSize(int size) const = 0;
+  virtual bool DistanceOK(double target_mul) const = 0;
+  virtual float distmap_aggregate() const = 0;
+  virtual const std::vector<float>& block_max_distance() const = 0;
+  virtual float BlockErrorLimit() const = 0;
+  virtual void ComputeBlockErrorAdjustmentWeights(int direction, int max_block_dist,
+                                                  double target_mul, int factor_x, int factor_y,
+                                                  const std::vector<float>& max_dist_per_block,
+                                                  std::vector<float>* block_weight) = 0;
+  // Makes the q=1 coefficients of the original image available to
+  // QuantizeFromOriginal / BlockZeroingOrders.
+  virtual bool SetOriginalCoeffs(const JpegData& jpg) = 0;
+  virtual const std::string& error() const = 0;
+};
+
+// ComputeBlockErrorAdjustmentWeights of butteraugli_comparator.cc:169-233
+// given the per-block maxima of the distance map.
+void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int max_block_dist,
+                                 double target_mul, int factor_x, int factor_y,
+                                 const std::vector<float>& max_dist_per_block,
+                                 std::vector<float>* block_weight);
+
+// guetzli::ButteraugliComparator on the HIP engine.
+class HipButteraugliComparator : public Comparator {
+ public:
+  static std::unique_ptr<HipButteraugliComparator> Create(int device, int w, int h,
+                                                          const uint8_t* rgb, bool device_ptr,
+                                                          float target, std::string* err);
+  bool Compare(const CoeffImage& img) override;
+  bool StartBlockComparisons() override;
+  void FinishBlockComparisons() override {}
+  bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
+                          int lookahead, std::vector<CoeffData>* out) override;
+  bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) override;
+  double ScoreOutputSize(int size) const override;
+  bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }
+  float distmap_aggregate() const override { return distance_; }
+  const std::vector<float>& block_max_distance() const override { return block_max_; }
+  float BlockErrorLimit() const override { return target_; }
+  void ComputeBlockErrorAdjustmentWeights(int direction, int max_block_dist, double target_mul,
+                                          int factor_x, int factor_y,
+                                          const std::vector<float>& max_dist_per_block,
+                                          std::vector<float>* block_weight) override;
+  const std::string& error() const override { return err_; }
+  bool SetOriginalCoeffs(const JpegData& jpg) override;
+  Engine* engine() { return engine_.get(); }
+  double seconds_compare = 0.0;
+  double seconds_zeroing = 0.0;
+  int compares = 0;
+
+ private:
+  std::unique_ptr<Engine> engine_;
+  int w_ = 0, h_ = 0;
+  float target_ = 0.0f;
+  float distance_ = 0.0f;
+  std::vector<float> block_max_;
+  uint64_t device_version_ = ~0ull;  // CoeffImage::version mirrored on device
+  std::string err_;
+};
+
+struct ProcessParams {  // guetzli::Params, processor.h:34-42 (4:4:4 subset)
+  float butteraugli_target = 1.0f;
+  bool clear_metadata = true;
+  int zeroing_greedy_lookahead = 3;
+  bool new_zeroing_model = true;
+};
+
+struct ProcessResult {
+  std::string jpeg;
+  int iterations = 0, iterations_up = 0, iterations_down = 0, compares = 0;
+  double seconds_compare = 0.0, seconds_zeroing = 0.0, seconds_total = 0.0;
+};
+
+// guetzli::Process(params, stats, rgb, w, h, &out) (processor.cc:1157-1185).
+// Returns 0 or a gz_status error code.
+int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool device_ptr, int w,
+            int h, ProcessResult* result, std::string* err);
+
+// The q=1 4:4:4 JPEG model of an RGB image (EncodeRGBToJpeg).
+void EncodeRGBToJpegData(const uint8_t* rgb, int w, int h, JpegData* jpg);
+
+// guetzli::ProcessJpegData (processor.cc:931-1020) with any comparator
+// (nullptr: image too small for Butteraugli).  Returns 0 or a gz_status.
+int ProcessJpegData(const ProcessParams& params, const JpegData& jpg, Comparator* cmp,
+                    ProcessResult* result, std::string* err);
+
+}  // namespace gz

@@ -1,0 +1,492 @@
+// The single device translation unit of libguetzli_hip: constant tables,
+// all kernels (included .inc files) and the Engine that sequences them.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off
+//        -fno-gpu-flush-denormals-to-zero (see csrc/Makefile).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../runtime/engine.h"
+#include "gz_math.h"
+
+namespace gz {
+__constant__ GzTables c_tab;
+}
+
+#include "butteraugli_kernels.inc"
+#include "block_zeroing.inc"
+#include "coeff_kernels.inc"
+
+namespace gz {
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Host-side table construction (glibc exp/pow in double, as the reference).
+// ---------------------------------------------------------------------------
+
+const float kZeroingCsf[192] = {
+#include "../host/zeroing_csf.inc"
+};
+
+const double kBlockCsfD[37] = {
+    5.28270670524, 0.0, 0.0, 0.0, 0.3831134973, 0.676303603859, 3.58927792424, 18.6104367002,
+    18.6104367002, 3.09093131948, 1.0, 0.498250875965, 0.36198671102, 0.308982169883,
+    0.1312701920435, 2.37370549629, 3.58927792424, 1.0, 2.37370549629, 0.991205724152,
+    1.05178802919, 0.627264168628, 0.4, 0.1312701920435, 0.676303603859, 0.498250875965,
+    0.991205724152, 0.5, 0.3831134973, 0.349686450518, 0.627264168628, 0.308982169883,
+    0.3831134973, 0.36198671102, 1.05178802919, 0.3831134973, 0.12,
+};
+
+const int kIdct[64] = {
+    8192, 11363, 10703, 9633,   8192,  6437,   4433,   2260,   8192, 9633,  4433,  -2259, -8192,
+    -11362, -10704, -6436, 8192, 6437, -4433,  -11362, -8192, 2261,   10704,  9633, 8192,  2260,
+    -10703, -6436, 8192, 9633,  -4433, -11363, 8192,   -2260, -10703, 6436,   8192, -9633, -4433,
+    11363,  8192,  -6437, -4433, 11362, -8192, -2261,  10704, -9633,  8192,   -9633, 4433, 2259,
+    -8192,  11362, -10704, 6436, 8192,  -11363, 10703, -9633, 8192,   -6437,  4433,  -2260,
+};
+
+// (extmul, extoff, offset, scaler, mul) of MaskX..MaskDcB, clbutter_comparator.cpp:994-1064
+const float kMaskParams[6][5] = {
+    {0.975741017749f, -4.25328244168f, 0.454909521427f, 0.0738288224836f, 20.8029176447f},
+    {0.373995618954f, 1.5307267433f, 0.911952641929f, 1.1731667845f, 16.2447033988f},
+    {0.61582234137f, -4.25376118646f, 1.05105070921f, 0.47434643535f, 31.1444967089f},
+    {1.79116943438f, -3.86797479189f, 0.670960225853f, 0.486575865525f, 20.4563479139f},
+    {0.212223514236f, -3.65647120524f, 1.73396799447f, 0.170392660501f, 21.6566724788f},
+    {0.349376011816f, -0.894711072781f, 0.901647926679f, 0.380086095024f, 18.0373825149f},
+};
+
+int Fix16(double x) { return static_cast<int>(x * 65536.0 + 0.5); }
+
+void BuildBlur(float sigma, float border_ratio, BlurSpec* b) {
+  // BlurOpt tap construction, clbutter_comparator.cpp:60-69
+  const float m = 2.25f;
+  const float scaler = static_cast<float>(-1.0 / (2 * sigma * sigma));
+  int diff = static_cast<int>(m * fabsf(sigma));
+  if (diff < 1) diff = 1;
+  b->radius = diff;
+  for (int i = -diff; i <= diff; ++i)
+    b->taps[i + diff] = static_cast<float>(exp(static_cast<double>(scaler * i * i)));
+  int step = static_cast<int>(sigma / 3);
+  b->step = step < 1 ? 1 : step;
+  b->border_ratio = border_ratio;
+  float wnb = 0.0f;
+  for (int j = 0; j <= 2 * diff; ++j) wnb += b->taps[j];
+  b->weight_no_border = wnb;
+}
+
+void BuildTables(GzTables* t) {
+  memset(t, 0, sizeof(*t));
+  for (int i = 0; i < 256; ++i) {
+    const double lin =
+        i < 11 ? i / 12.92 : 255.0 * pow(((i / 255.0) + 0.055) / 1.055, 2.4);  // gamma_correct.cc:27-33
+    t->srgb[i] = static_cast<float>(lin);
+    const int x = i - 128;  // libjpeg build_ycc_rgb_table (color_transform.h tables)
+    t->cr_r[i] = (Fix16(1.40200) * x + 32768) >> 16;
+    t->cb_b[i] = (Fix16(1.77200) * x + 32768) >> 16;
+    t->cr_g[i] = -Fix16(0.71414) * x;
+    t->cb_g[i] = -Fix16(0.34414) * x + 32768;
+  }
+  t->hf_dx[0] = 0.0f; t->hf_dx[1] = 11.38708334481672f;
+  t->hf_dy[0] = 0.0f; t->hf_dy[1] = 1.4103373714040413f;
+  t->lf_dy[0] = 0.0f;
+  for (int i = 2; i < 21; ++i) {
+    t->hf_dx[i] = t->hf_dx[i - 1] + 14.550189611520716f;
+    t->hf_dy[i] = t->hf_dy[i - 1] + 0.7084088867024f;
+  }
+  for (int i = 1; i < 21; ++i) t->lf_dy[i] = t->lf_dy[i - 1] + 5.2511644570349185f;
+  t->hf_dy_d[0] = 0.0; t->hf_dy_d[1] = 1.4103373714040413;
+  for (int i = 2; i < 21; ++i) t->hf_dy_d[i] = t->hf_dy_d[i - 1] + 0.7084088867024;
+  t->lf_dy_d[0] = 0.0;
+  for (int i = 1; i < 21; ++i) t->lf_dy_d[i] = t->lf_dy_d[i - 1] + 5.2511644570349185;
+  for (int m = 0; m < 6; ++m) {
+    const float extmul = kMaskParams[m][0], extoff = kMaskParams[m][1];
+    const float offset = kMaskParams[m][2], scaler = kMaskParams[m][3], mul = kMaskParams[m][4];
+    for (size_t i = 0; i < 512; ++i) {
+      const float c = static_cast<float>(mul / ((0.01 * scaler * i) + offset));
+      const float v = static_cast<float>(1.0 + extmul * (c + extoff));
+      t->mask_lut[m][i] = v * v;
+    }
+  }
+  for (int i = 0; i < 37; ++i) {
+    t->block_csf[i] = static_cast<float>(kBlockCsfD[i]);
+    t->block_csf_d[i] = kBlockCsfD[i];
+  }
+  memcpy(t->zeroing_csf, kZeroingCsf, sizeof(kZeroingCsf));
+  memcpy(t->idct, kIdct, sizeof(kIdct));
+  BuildBlur(1.1f, 0.0f, &t->blur[kSigOpsin]);
+  BuildBlur(1.5f, 0.0f, &t->blur[kSigEdgeX]);
+  BuildBlur(0.586f, 0.0f, &t->blur[kSigEdgeY]);
+  BuildBlur(0.4f, 0.0f, &t->blur[kSigEdgeB]);
+  BuildBlur(14.0f, 0.0f, &t->blur[kSigLowFreq]);
+  BuildBlur(9.65781083553f, 0.0f, &t->blur[kSigMaskX]);
+  BuildBlur(14.2644604355f, 0.0f, &t->blur[kSigMaskY]);
+  BuildBlur(4.53358927369f, 0.0f, &t->blur[kSigMaskB]);
+  BuildBlur(8.8510880283f, 0.03027655136f, &t->blur[kSigDiffmap]);
+}
+
+std::mutex g_tab_mu;
+bool g_tab_uploaded[64] = {false};
+GzTables* g_host_tab = nullptr;
+
+const GzTables& HostTables() {
+  // called under g_tab_mu
+  if (!g_host_tab) {
+    g_host_tab = new GzTables;
+    BuildTables(g_host_tab);
+  }
+  return *g_host_tab;
+}
+
+inline dim3 PixGrid(int w, int h, int planes = 1) {
+  return dim3((w + 255) / 256, h, planes);
+}
+
+}  // namespace
+
+#define GZ_HIP(call)                                   \
+  do {                                                 \
+    hipError_t e_ = (call);                            \
+    if (e_ != hipSuccess) return Fail(#call, (int)e_); \
+  } while (0)
+#define GZ_LAUNCH()                                               \
+  do {                                                            \
+    hipError_t e_ = hipGetLastError();                            \
+    if (e_ != hipSuccess) return Fail("kernel launch", (int)e_);  \
+  } while (0)
+
+bool Engine::Fail(const char* what, int code) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s failed: %s (%d)", what,
+           hipGetErrorString(static_cast<hipError_t>(code)), code);
+  err_ = buf;
+  return false;
+}
+
+std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* err) {
+  std::unique_ptr<Engine> e(new Engine);
+  auto fail = [&](const std::string& m) {
+    if (err) *err = m;
+    return std::unique_ptr<Engine>();
+  };
+  if (w < 8 || h < 8 || w >= (1 << 16) || h >= (1 << 16)) return fail("unsupported image size");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail("no HIP device available");
+  if (device < 0 || device >= ndev || device >= 64) return fail("bad device index");
+  if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+  {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    if (!g_tab_uploaded[device]) {
+      const GzTables& t = HostTables();
+      if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(t)) != hipSuccess)
+        return fail("table upload failed");
+      g_tab_uploaded[device] = true;
+    }
+  }
+  e->device_ = device;
+  e->w_ = w;
+  e->h_ = h;
+  e->bw_ = (w + 7) / 8;
+  e->bh_ = (h + 7) / 8;
+  e->nb_ = e->bw_ * e->bh_;
+  e->rw_ = (w + 2) / 3;
+  e->rh_ = (h + 2) / 3;
+  e->n_ = static_cast<size_t>(w) * h;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  e->stream_ = s;
+  const size_t n = e->n_, rn = static_cast<size_t>(e->rw_) * e->rh_;
+  const size_t nc = static_cast<size_t>(e->nb_) * 64 * 3;
+  bool ok = true;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (ok && hipMalloc(p, bytes) != hipSuccess) ok = false;
+  };
+  alloc(reinterpret_cast<void**>(&e->d_rgb_), 3 * n);
+  alloc(reinterpret_cast<void**>(&e->d_orig_), nc * sizeof(int16_t));
+  alloc(reinterpret_cast<void**>(&e->d_cur_), nc * sizeof(int16_t));
+  alloc(reinterpret_cast<void**>(&e->d_ref_xyb_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_lin_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_xyb_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_m0_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_m1_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_tmp_), 6 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_bl_), 6 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_ma_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_mb_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_edge_), 3 * rn * 4);
+  alloc(reinterpret_cast<void**>(&e->d_dc_), 3 * rn * 4);
+  alloc(reinterpret_cast<void**>(&e->d_ac_), 3 * rn * 4);
+  alloc(reinterpret_cast<void**>(&e->d_resval_), rn * 4);
+  alloc(reinterpret_cast<void**>(&e->d_dd_), n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_block_max_), e->nb_ * 4);
+  alloc(reinterpret_cast<void**>(&e->d_gmax_), 16);
+  alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
+  alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_gmax_), 16) != hipSuccess) ok = false;
+  if (!ok) return fail("device allocation failed");
+  return e;
+}
+
+Engine::~Engine() {
+  if (device_ >= 0) hipSetDevice(device_);
+  void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
+                  d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
+                  d_dd_, d_block_max_, d_gmax_, d_mask_scale_, d_zero_out_};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (h_gmax_) hipHostFree(h_gmax_);
+  if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
+}
+
+bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  GZ_HIP(hipMemcpyAsync(d_rgb_, rgb, 3 * n_, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_rgb_, n_, d_lin_);
+  GZ_LAUNCH();
+  BlurPlanes bp{};
+  for (int c = 0; c < 3; ++c) {
+    bp.in[c] = d_lin_ + c * n_;
+    bp.out[c] = d_tmp_ + c * n_;
+    bp.sig[c] = kSigOpsin;
+  }
+  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_);
+  GZ_LAUNCH();
+  GZ_HIP(hipStreamSynchronize(s));
+  have_mask_scale_ = false;
+  return true;
+}
+
+bool Engine::SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  GZ_HIP(hipMemcpyAsync(d_orig_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
+                        device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::UploadCoeffs(const int16_t* coeffs) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  GZ_HIP(hipMemcpyAsync(d_cur_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
+                        hipMemcpyHostToDevice, s));
+  return true;
+}
+
+bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  QuantMatrix qm;
+  memcpy(qm.q, q, sizeof(qm.q));
+  const size_t per = static_cast<size_t>(nb_) * 64;
+  k_quantize<<<dim3((per + 255) / 256, 3), 256, 0, s>>>(d_orig_, qm, per, d_cur_);
+  GZ_LAUNCH();
+  if (host_out) {
+    GZ_HIP(hipMemcpyAsync(host_out, d_cur_, 3 * per * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+    GZ_HIP(hipStreamSynchronize(s));
+  }
+  return true;
+}
+
+bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  k_diff_precompute<<<PixGrid(w_, h_), 256, 0, s>>>(xyb0, xyb1, w_, h_, d_ma_);
+  GZ_LAUNCH();
+  k_average5x5<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_);
+  GZ_LAUNCH();
+  k_min4_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_mb_, w_, h_, d_ma_);
+  GZ_LAUNCH();
+  k_min4_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_);
+  GZ_LAUNCH();
+  BlurPlanes bp{};
+  for (int c = 0; c < 3; ++c) {
+    bp.in[c] = d_mb_ + c * n_;
+    bp.out[c] = d_tmp_ + c * n_;
+    bp.sig[c] = kSigMaskX + c;
+  }
+  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  for (int c = 0; c < 3; ++c) {
+    bp.in[c] = d_tmp_ + c * n_;
+    bp.out[c] = d_ma_ + c * n_;
+  }
+  k_blur_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  return true;
+}
+
+bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  const size_t n = n_, rn = static_cast<size_t>(rw_) * rh_;
+  auto d2h = [&](float* dst, const float* src, size_t count) -> bool {
+    if (!dst) return true;
+    GZ_HIP(hipMemcpyAsync(dst, src, count * 4, hipMemcpyDeviceToHost, s));
+    return true;
+  };
+  GZ_HIP(hipMemsetAsync(d_edge_, 0, 3 * rn * 4, s));
+  GZ_HIP(hipMemsetAsync(d_dc_, 0, 3 * rn * 4, s));
+  GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
+  GZ_HIP(hipMemsetAsync(d_gmax_, 0, 4, s));
+  // S0: candidate coefficients -> linear RGB
+  k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_);
+  GZ_LAUNCH();
+  if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
+  // S1/S2: opsin dynamics
+  BlurPlanes bp{};
+  for (int c = 0; c < 3; ++c) {
+    bp.in[c] = d_lin_ + c * n;
+    bp.out[c] = d_tmp_ + c * n;
+    bp.sig[c] = kSigOpsin;
+  }
+  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_);
+  GZ_LAUNCH();
+  if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
+  // S3: high intensity change masking
+  k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_);
+  GZ_LAUNCH();
+  if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
+  if (dbg && !d2h(dbg->mhic1, d_m1_, 3 * n)) return false;
+  // S4/S5: edge detector map
+  for (int c = 0; c < 3; ++c) {
+    const int sig = kSigEdgeX + c;
+    bp.in[c] = d_m0_ + c * n;
+    bp.in[3 + c] = d_m1_ + c * n;
+    bp.out[c] = d_tmp_ + c * n;
+    bp.out[3 + c] = d_tmp_ + (3 + c) * n;
+    bp.sig[c] = sig;
+    bp.sig[3 + c] = sig;
+  }
+  k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  for (int p = 0; p < 6; ++p) {
+    bp.in[p] = d_tmp_ + p * n;
+    bp.out[p] = d_bl_ + p * n;
+  }
+  k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_);
+  GZ_LAUNCH();
+  if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
+  // S6: block diff
+  k_block_diff<<<(static_cast<unsigned>(rn) + kBdPoints - 1) / kBdPoints, 256, 0, s>>>(
+      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_);
+  GZ_LAUNCH();
+  if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
+  if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
+  // S7/S8: low-frequency edge term (sigma 14, step 4)
+  for (int c = 0; c < 3; ++c) {
+    bp.in[c] = d_m0_ + c * n;
+    bp.in[3 + c] = d_m1_ + c * n;
+    bp.sig[c] = kSigLowFreq;
+    bp.sig[3 + c] = kSigLowFreq;
+  }
+  for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
+  k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
+  GZ_LAUNCH();
+  {
+    const int st = HostTables().blur[kSigLowFreq].step;
+    const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
+    for (int p = 0; p < 6; ++p) {
+      bp.in[p] = d_tmp_ + p * n;
+      bp.out[p] = d_bl_ + p * dn;
+    }
+    k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
+    GZ_LAUNCH();
+    k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_);
+    GZ_LAUNCH();
+  }
+  if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
+  // S9-S13: activity mask
+  if (!MaskPipeline(d_m0_, d_m1_)) return false;
+  MaskPlanes mk{{d_ma_, d_ma_ + n, d_ma_ + 2 * n}};
+  if (dbg && (dbg->mask || dbg->mask_dc)) {
+    k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_);
+    GZ_LAUNCH();
+    if (!d2h(dbg->mask, d_mb_, 3 * n)) return false;
+    if (!d2h(dbg->mask_dc, d_tmp_, 3 * n)) return false;
+  }
+  // S14/S15: combine channels (+ mask LUTs, + sqrt)
+  float* dbg_comb = nullptr;
+  if (dbg && dbg->combined) dbg_comb = d_bl_;  // scratch, consumed below
+  k_combine<<<PixGrid(rw_, rh_), 256, 0, s>>>(mk, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_,
+                                               d_resval_, dbg_comb);
+  GZ_LAUNCH();
+  if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
+  // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
+  {
+    const int wc = w_ - 5, hc = h_ - 5;
+    const int st = HostTables().blur[kSigDiffmap].step;
+    const int dxc = (wc + st - 1) / st;
+    k_diffmap_blur_h<<<PixGrid(dxc, hc), 256, 0, s>>>(d_resval_, rw_, wc, hc, d_tmp_);
+    GZ_LAUNCH();
+    BlurPlanes bd{};
+    bd.in[0] = d_tmp_;
+    bd.out[0] = d_dd_;
+    bd.sig[0] = kSigDiffmap;
+    k_blur_v<<<PixGrid(dxc, hc), 256, 0, s>>>(bd, wc, hc);
+    GZ_LAUNCH();
+    float* dm = nullptr;
+    if (dbg && dbg->distmap) dm = d_bl_;
+    k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
+                                                              dm, d_block_max_, d_gmax_);
+    GZ_LAUNCH();
+    if (dm && !d2h(dbg->distmap, dm, n)) return false;
+  }
+  GZ_HIP(hipMemcpyAsync(h_gmax_, d_gmax_, 4, hipMemcpyDeviceToHost, s));
+  if (block_max) GZ_HIP(hipMemcpyAsync(block_max, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  float d;
+  memcpy(&d, h_gmax_, 4);
+  *distance = d;
+  return true;
+}
+
+bool Engine::StartBlockComparisons(float* mask_scale_host) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  // ButteraugliComparator::StartBlockComparisons: Mask(rgb0, rgb0) with no
+  // high-intensity masking (butteraugli_comparator.cc:72-79).
+  if (!MaskPipeline(d_ref_xyb_, d_ref_xyb_)) return false;
+  MaskPlanes mk{{d_ma_, d_ma_ + n_, d_ma_ + 2 * n_}};
+  k_mask_scale<<<(nb_ + 255) / 256, 256, 0, s>>>(mk, w_, h_, bw_, nb_, d_mask_scale_);
+  GZ_LAUNCH();
+  if (mask_scale_host)
+    GZ_HIP(hipMemcpyAsync(mask_scale_host, d_mask_scale_, 3 * nb_ * 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  have_mask_scale_ = true;
+  return true;
+}
+
+bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+                                     comp_mask, limit, lookahead,
+                                     static_cast<CoeffData*>(d_zero_out_));
+  GZ_LAUNCH();
+  GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
+                        hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  return true;
+}
+
+double Engine::last_kernel_ms(const char*) const { return 0.0; }
+
+const char* BuildInfo() {
+  return "libguetzli_hip (gfx950)";
+}
+
+}  // namespace gz

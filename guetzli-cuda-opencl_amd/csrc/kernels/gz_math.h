@@ -1,0 +1,345 @@
+// Device-side scalar math of the Butteraugli `--c` path, shared by the
+// full-image Compare kernels and the per-block zeroing kernel.
+//
+// Numerics contract: every function reproduces the
+// float/double promotion of the reference source it cites.  The library is
+// built with -ffp-contract=off, IEEE f32 denormals and correctly rounded f32
+// div/sqrt, so each scalar op rounds exactly like the x86 SSE oracle.
+// Transcendental tables (blur taps, sRGB, mask LUTs) are computed on the host
+// with glibc and live in GzTables (constant memory).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gz {
+
+constexpr int kMaxTaps = 72;   // largest blur: sigma 14.26 -> 65 taps
+constexpr int kNumSigmas = 9;
+
+// Blur kernels used by the path (clbutter_comparator.cpp:57-94 callers).
+enum SigmaId : int {
+  kSigOpsin = 0,   // 1.1      OpsinDynamicsImageOpt           :885
+  kSigEdgeX = 1,   // 1.5      EdgeDetectorMapOpt              :1460
+  kSigEdgeY = 2,   // 0.586
+  kSigEdgeB = 3,   // 0.4
+  kSigLowFreq = 4, // 14       EdgeDetectorLowFreqOpt          :1491
+  kSigMaskX = 5,   // 9.65781083553   MaskOpt                  :1227
+  kSigMaskY = 6,   // 14.2644604355
+  kSigMaskB = 7,   // 4.53358927369
+  kSigDiffmap = 8, // 8.8510880283 (border_ratio 0.03027655136) CalculateDiffmapOpt :958
+};
+
+struct BlurSpec {
+  int radius;          // "diff" in BlurOpt
+  int step;            // xstep == ystep
+  float border_ratio;
+  float weight_no_border;
+  float taps[kMaxTaps];  // expn[0 .. 2*radius]
+};
+
+struct GzTables {
+  float srgb[256];          // (float)Srgb8ToLinearTable()[i]   gamma_correct.cc:23-38
+  int cr_r[256], cb_b[256], cr_g[256], cb_g[256];  // color_transform.h
+  float hf_dx[21], hf_dy[21], lf_dy[21];           // clbutter_comparator.cpp:146-193
+  double hf_dy_d[21], lf_dy_d[21];                 // butteraugli.cc:217-247
+  float mask_lut[6][512];                          // clbutter_comparator.cpp:980-1064
+  float block_csf[37];                             // :103-144
+  double block_csf_d[37];                          // butteraugli.cc:157-198
+  float zeroing_csf[192];                          // order.inc:3
+  int idct[64];                                    // idct.cc:29-38
+  BlurSpec blur[kNumSigmas];
+};
+
+// Planes handled by one launch of the separable blur (blockIdx.z = plane).
+struct BlurPlanes {
+  const float* in[6];
+  float* out[6];
+  int sig[6];
+};
+
+// Defined once in gz_device.hip (the single device translation unit).
+extern __constant__ GzTables c_tab;
+
+// ---------------------------------------------------------------------------
+// Small helpers
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ float interp_f(const float* a, int size, float sx) {
+  // InterpolateOpt, clbutter_comparator.cpp:195-210
+  const float ix = fabsf(sx);
+  const int base = static_cast<int>(ix);
+  float res;
+  if (base >= size - 1) {
+    res = a[size - 1];
+  } else {
+    const float mix = ix - base;
+    res = a[base] + mix * (a[base + 1] - a[base]);
+  }
+  return sx < 0 ? -res : res;
+}
+
+__device__ __forceinline__ float interp_clamp_neg_f(const float* a, int size, float sx) {
+  // InterpolateClampNegativeOpt, :212-229
+  if (sx < 0) sx = 0;
+  const float ix = fabsf(sx);
+  const int base = static_cast<int>(ix);
+  if (base >= size - 1) return a[size - 1];
+  const float mix = ix - base;
+  return a[base] + mix * (a[base + 1] - a[base]);
+}
+
+__device__ __forceinline__ double interp_d(const double* a, int size, double sx) {
+  // Interpolate, butteraugli.cc:249-263
+  const double ix = fabs(sx);
+  const int base = static_cast<int>(ix);
+  double res;
+  if (base >= size - 1) {
+    res = a[size - 1];
+  } else {
+    const double mix = ix - base;
+    res = a[base] + mix * (a[base + 1] - a[base]);
+  }
+  return sx < 0 ? -res : res;
+}
+
+// XybLowFreqToValsOpt + XybDiffLowFreqSquaredAccumulateOpt with the second
+// colour == 0 (the only form used on the path), :253-299.
+__device__ __forceinline__ void lowfreq_sq_zero_f(float x, float y, float z, float factor,
+                                                  float res[3]) {
+  z += 0.0812519812628f * y;
+  const float vz = z * 7.34905756986f;
+  const float vx = x * 6.64482198135f;
+  const float vy = interp_f(c_tab.lf_dy, 21, y * 0.837846224276f);
+  res[0] += factor * vx * vx;
+  res[1] += factor * vy * vy;
+  res[2] += factor * vz * vz;
+}
+
+__device__ __forceinline__ void lowfreq_vals_f(float x, float y, float z, float v[3]) {
+  z += 0.0812519812628f * y;
+  v[2] = z * 7.34905756986f;
+  v[0] = x * 6.64482198135f;
+  v[1] = interp_f(c_tab.lf_dy, 21, y * 0.837846224276f);
+}
+
+// General two-colour form (used by the corner edge detector).
+__device__ __forceinline__ void lowfreq_sq_f(const float a[3], const float b[3], float factor,
+                                             float res[3]) {
+  float v0[3];
+  lowfreq_vals_f(a[0], a[1], a[2], v0);
+  if (b[0] == 0.0f && b[1] == 0.0f && b[2] == 0.0f) {
+    res[0] += factor * v0[0] * v0[0];
+    res[1] += factor * v0[1] * v0[1];
+    res[2] += factor * v0[2] * v0[2];
+    return;
+  }
+  float v1[3];
+  lowfreq_vals_f(b[0], b[1], b[2], v1);
+  const float dx = v0[0] - v1[0], dy = v0[1] - v1[1], dz = v0[2] - v1[2];
+  res[0] += factor * dx * dx;
+  res[1] += factor * dy * dy;
+  res[2] += factor * dz * dz;
+}
+
+__device__ __forceinline__ void lowfreq_sq_zero_d(double x, double y, double z, double factor,
+                                                  double res[3]) {
+  // butteraugli.cc:305-340 (double)
+  z += 0.0812519812628 * y;
+  const double vz = z * 7.34905756986;
+  const double vx = x * 6.64482198135;
+  const double vy = interp_d(c_tab.lf_dy_d, 21, y * 0.837846224276);
+  res[0] += factor * vx * vx;
+  res[1] += factor * vy * vy;
+  res[2] += factor * vz * vz;
+}
+
+template <typename T>
+__device__ __forceinline__ T remove_range(T v, T range) {
+  if (v >= -range && v < range) return 0;
+  return v < 0 ? v + range : v - range;
+}
+
+// ---------------------------------------------------------------------------
+// Opsin dynamics per pixel (clbutter_comparator.cpp:708-912)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void opsin_absorbance(float r, float g, float b, float out[3]) {
+  out[0] = 0.348036746003f * r + 0.577814843137f * g + 0.0544556093735f * b + 0.774145581713f;
+  out[1] = 0.26922717275f * r + 0.767247733938f * g + 0.0366922708552f * b + 0.920130265014f;
+  out[2] = 0.0882062883536f * r + 0.158581714673f * g + 0.712857943858f * b + 10.6524069248f;
+}
+
+__device__ __forceinline__ float clenshaw6(float x, float c0, float c1, float c2, float c3,
+                                           float c4, float c5) {
+  // ClenshawRecursionOpt<5..0>, :806-824
+  float b1 = 0.0f, b2 = 0.0f, xb, t;
+  xb = x * b1; t = (xb + xb) - b2 + c5; b2 = b1; b1 = t;
+  xb = x * b1; t = (xb + xb) - b2 + c4; b2 = b1; b1 = t;
+  xb = x * b1; t = (xb + xb) - b2 + c3; b2 = b1; b1 = t;
+  xb = x * b1; t = (xb + xb) - b2 + c2; b2 = b1; b1 = t;
+  xb = x * b1; t = (xb + xb) - b2 + c1; b2 = b1; b1 = t;
+  xb = x * b1;
+  return xb - b2 + c0;
+}
+
+__device__ __forceinline__ float gamma_poly(float x) {
+  // GammaPolynomialOpt, :861-874 (RationalPolynomialOpt :828-859)
+  const float lo = 0.770000000000000f, hi = 274.579999999999984f;
+  const float x01 = (x - lo) / (hi - lo);
+  const float xc = static_cast<float>(2.0 * static_cast<double>(x01) - 1.0);
+  const float yp = clenshaw6(xc, 881.979476556478289f, 1496.058452015812463f,
+                             908.662212739659481f, 373.566100223287378f, 85.840860336314364f,
+                             6.683258861509244f);
+  const float yq = clenshaw6(xc, 12.262350348616792f, 20.557285797683576f,
+                             12.161463238367844f, 4.711532733641639f, 0.899112889751053f,
+                             0.035662329617191f);
+  if (yq == 0.0f) return 0.0f;
+  return yp / yq;
+}
+
+// blurred: sigma-1.1 blur of the linear pixel; lin: the linear pixel.
+__device__ __forceinline__ void opsin_pixel(const float blurred[3], const float lin[3],
+                                            float xyb[3]) {
+  float pm[3], sens[3], cm[3];
+  opsin_absorbance(blurred[0], blurred[1], blurred[2], pm);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) sens[c] = gamma_poly(pm[c]) / pm[c];
+  opsin_absorbance(lin[0], lin[1], lin[2], cm);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) cm[c] *= sens[c];
+  xyb[0] = 1.01611726948f * cm[0] - 0.982482243696f * cm[1];
+  xyb[1] = 1.43571362627f * cm[0] + 0.896039849412f * cm[1];
+  xyb[2] = cm[2];
+}
+
+// MaskHighIntensityChangeOpt mixing for one pixel, :739-778.
+// sqr_max_diff is the max over valid 4-neighbours of
+// float(0.5*(c0y[n]+c1y[n]) - ave_y)^2, or -1 when none.
+__device__ __forceinline__ float mhic_ave(float a, float b) {
+  return static_cast<float>((static_cast<double>(a + b)) * 0.5);
+}
+__device__ __forceinline__ float mhic_sqdiff(float n0, float n1, float ave_y) {
+  float d = static_cast<float>(0.5 * static_cast<double>(n0 + n1) - static_cast<double>(ave_y));
+  return d * d;
+}
+__device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], const float ave[3],
+                                         float sqr_max_diff, float x0[3], float x1[3]) {
+  const float kRX = 275.19165240059317f, kRY = 18599.41286306991f;
+  const float kRZ = 410.8995306951065f, kChroma = 106.95800948271017f;
+  const float chroma_scale = kChroma / (ave[1] + kChroma);
+  const float mix[3] = {chroma_scale * kRX / (sqr_max_diff + kRX), kRY / (sqr_max_diff + kRY),
+                        chroma_scale * kRZ / (sqr_max_diff + kRZ)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    x0[c] = mix[c] * c0[c] + (1 - mix[c]) * ave[c];
+    x1[c] = mix[c] * c1[c] + (1 - mix[c]) * ave[c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Colour conversion (color_transform.h:211-218) and sRGB -> linear
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+__device__ __forceinline__ void ycbcr_to_linear(int y, int cb, int cr, float out[3]) {
+  const int r = clamp255(y + c_tab.cr_r[cr]);
+  const int g = clamp255(y + ((c_tab.cr_g[cr] + c_tab.cb_g[cb]) >> 16));
+  const int b = clamp255(y + c_tab.cb_b[cb]);
+  out[0] = c_tab.srgb[r];
+  out[1] = c_tab.srgb[g];
+  out[2] = c_tab.srgb[b];
+}
+
+// ---------------------------------------------------------------------------
+// Mask LUT stage at one pixel (MaskOpt tail, :1234-1263)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void mask_luts(float s0, float s1, float s2, float mask[3],
+                                          float mask_dc[3]) {
+  const float p0 = 232.206464018f * s0, p1 = 22.9455222245f * s1, p2 = 503.962310606f * s2;
+  const float gs = static_cast<float>(1.0 / static_cast<double>(14.921561160295326f));
+  const float gs2 = gs * gs;
+  mask[0] = interp_clamp_neg_f(c_tab.mask_lut[0], 512, p0) * gs2;
+  mask[1] = interp_clamp_neg_f(c_tab.mask_lut[1], 512, p1) * gs2;
+  mask[2] = interp_clamp_neg_f(c_tab.mask_lut[2], 512, p2) * gs2;
+  mask_dc[0] = interp_clamp_neg_f(c_tab.mask_lut[3], 512, p0) * gs2;
+  mask_dc[1] = interp_clamp_neg_f(c_tab.mask_lut[4], 512, p1) * gs2;
+  mask_dc[2] = interp_clamp_neg_f(c_tab.mask_lut[5], 512, p2) * gs2;
+}
+
+// ---------------------------------------------------------------------------
+// 8-point FFTs (DJB in-place FFT used by butteraugli; the exact butterfly
+// sequence of clbutter_comparator.cpp:320-519 / butteraugli.cc:371-570).
+// Operates on split re/im arrays of 8.
+// ---------------------------------------------------------------------------
+
+template <typename T>
+__device__ __forceinline__ void fft_reorder8(T* re, T* im) {
+  const T tr = re[2], ti = im[2];
+  re[2] = re[3]; im[2] = im[3];
+  re[3] = re[5]; im[3] = im[5];
+  re[5] = re[7]; im[5] = im[7];
+  re[7] = re[4]; im[7] = im[4];
+  re[4] = re[1]; im[4] = im[1];
+  re[1] = re[6]; im[1] = im[6];
+  re[6] = tr; im[6] = ti;
+}
+
+template <typename T>
+__device__ __forceinline__ void fft4_inplace(T* re, T* im) {
+  T t1, t2, t3, t4, t5, t6, t7, t8;
+  t5 = re[2]; t1 = re[0] - t5; t7 = re[3]; t5 += re[0]; t3 = re[1] - t7; t7 += re[1];
+  t8 = t5 + t7; re[0] = t8; t5 -= t7; re[1] = t5;
+  t6 = im[2]; t2 = im[0] - t6; t6 += im[0]; t5 = im[3];
+  im[2] = t2 + t3; t2 -= t3; im[3] = t2;
+  t4 = im[1] - t5; re[3] = t1 + t4; t1 -= t4; re[2] = t1;
+  t5 += im[1]; im[0] = t6 + t5; t6 -= t5; im[1] = t6;
+}
+
+template <typename T>
+__device__ __forceinline__ void fft8_inplace(T* re, T* im, T sqrt_half) {
+  T t1, t2, t3, t4, t5, t6, t7, t8;
+  t7 = im[4]; t4 = im[0] - t7; t7 += im[0]; im[0] = t7;
+  t8 = re[6]; t5 = re[2] - t8; t8 += re[2]; re[2] = t8;
+  t7 = im[6]; im[6] = t4 - t5; t4 += t5; im[4] = t4;
+  t6 = im[2] - t7; t7 += im[2]; im[2] = t7;
+  t8 = re[4]; t3 = re[0] - t8; t8 += re[0]; re[0] = t8;
+  re[4] = t3 - t6; t3 += t6; re[6] = t3;
+  t7 = re[5]; t3 = re[1] - t7; t7 += re[1]; re[1] = t7;
+  t8 = im[7]; t6 = im[3] - t8; t8 += im[3]; im[3] = t8;
+  t1 = t3 - t6; t3 += t6;
+  t7 = im[5]; t4 = im[1] - t7; t7 += im[1]; im[1] = t7;
+  t8 = re[7]; t5 = re[3] - t8; t8 += re[3]; re[3] = t8;
+  t2 = t4 - t5; t4 += t5;
+  t6 = t1 - t4; t8 = sqrt_half; t6 *= t8; re[5] = re[4] - t6;
+  t1 += t4; t1 *= t8; im[5] = im[4] - t1;
+  t6 += re[4]; re[4] = t6; t1 += im[4]; im[4] = t1;
+  t5 = t2 - t3; t5 *= t8; im[7] = im[6] - t5;
+  t2 += t3; t2 *= t8; re[7] = re[6] - t2;
+  t2 += re[6]; re[6] = t2; t5 += im[6]; im[6] = t5;
+  fft4_inplace(re, im);
+  fft_reorder8(re, im);
+}
+
+template <typename T>
+__device__ __forceinline__ void real_fft8(const T* in, T* re, T* im, T sqrt_half) {
+  T t1, t2, t3, t5, t6, t7, t8;
+  t8 = in[6]; t5 = in[2] - t8; t8 += in[2]; re[2] = t8; im[6] = -t5; im[4] = t5;
+  t8 = in[4]; t3 = in[0] - t8; t8 += in[0]; re[0] = t8; re[4] = t3; re[6] = t3;
+  t7 = in[5]; t3 = in[1] - t7; t7 += in[1]; re[1] = t7;
+  t8 = in[7]; t5 = in[3] - t8; t8 += in[3]; re[3] = t8;
+  t2 = -t5; t6 = t3 - t5; t8 = sqrt_half; t6 *= t8; re[5] = re[4] - t6;
+  t1 = t3 + t5; t1 *= t8; im[5] = im[4] - t1;
+  t6 += re[4]; re[4] = t6; t1 += im[4]; im[4] = t1;
+  t5 = t2 - t3; t5 *= t8; im[7] = im[6] - t5;
+  t2 += t3; t2 *= t8; re[7] = re[6] - t2;
+  t2 += re[6]; re[6] = t2; t5 += im[6]; im[6] = t5;
+  t5 = re[2]; t1 = re[0] - t5; t7 = re[3]; t5 += re[0]; t3 = re[1] - t7; t7 += re[1];
+  t8 = t5 + t7; re[0] = t8; t5 -= t7; re[1] = t5;
+  im[2] = t3; im[3] = -t3; re[3] = t1; re[2] = t1; im[0] = 0; im[1] = 0;
+  fft_reorder8(re, im);
+}
+
+}  // namespace gz

@@ -1,0 +1,113 @@
+// Device engine: one Butteraugli comparison context for one image size on
+// one GPU (one HIP stream, persistent HBM buffers sized at creation).
+//
+// Replaces the reference's per-call pooled allocations + synchronous
+// launches (clguetzli/cuguetzli.cpp, cumem_pool.cpp, ocu.cpp): every buffer
+// is allocated once in Create(), the reference image's XYB is cached, and a
+// Compare is one stream-ordered sequence of kernels followed by a single
+// small device->host copy (distance + per-block maxima).
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+
+namespace gz {
+
+struct CoeffDataHost {  // guetzli::CoeffData (processor.h:29-32)
+  int idx;
+  float block_err;
+};
+
+// Optional host destinations for stage-level parity tests.
+struct CompareDebug {
+  float* cand_linear = nullptr;   // 3*w*h
+  float* cand_xyb = nullptr;      // 3*w*h
+  float* mhic0 = nullptr;         // 3*w*h
+  float* mhic1 = nullptr;         // 3*w*h
+  float* edge = nullptr;          // 3*rw*rh
+  float* block_dc = nullptr;      // 3*rw*rh
+  float* block_ac = nullptr;      // 3*rw*rh (before the low-frequency term)
+  float* block_ac_lf = nullptr;   // 3*rw*rh
+  float* mask = nullptr;          // 3*w*h
+  float* mask_dc = nullptr;       // 3*w*h
+  float* combined = nullptr;      // rw*rh
+  float* distmap = nullptr;       // w*h
+};
+
+class Engine {
+ public:
+  // Returns nullptr and sets *err on failure.
+  static std::unique_ptr<Engine> Create(int device, int w, int h, std::string* err);
+  ~Engine();
+
+  int width() const { return w_; }
+  int height() const { return h_; }
+  int blocks() const { return nb_; }
+
+  // Reference image (RGB8 interleaved); computes and caches its XYB.
+  bool SetReference(const uint8_t* rgb, bool device_ptr);
+  // q=1 coefficients of the reference ([3][blocks][64]); kept resident.
+  bool SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr);
+  // Candidate coefficients ([3][blocks][64]).
+  bool UploadCoeffs(const int16_t* coeffs);
+  // cur = Quantize(orig, q) on device, copied back to host_out if non-null.
+  bool QuantizeFromOriginal(const int q[3][64], int16_t* host_out);
+
+  // Butteraugli distance of the current candidate.  block_max (blocks
+  // floats, may be null) receives the per-8x8 maximum of the distance map.
+  bool Compare(float* distance, float* block_max, CompareDebug* dbg);
+
+  // Mask(ref, ref) sampled at block corners (StartBlockComparisons).
+  bool StartBlockComparisons(float* mask_scale_host /* 3*blocks, may be null */);
+  // Per-block greedy zeroing orders for the current candidate.
+  bool BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out);
+
+  const std::string& error() const { return err_; }
+  void* stream() const { return stream_; }
+  double last_kernel_ms(const char* which) const;
+
+ private:
+  Engine() = default;
+  bool Fail(const char* what, int code);
+  bool MaskPipeline(const float* xyb0, const float* xyb1);
+
+  int device_ = 0;
+  int w_ = 0, h_ = 0, bw_ = 0, bh_ = 0, nb_ = 0, rw_ = 0, rh_ = 0;
+  size_t n_ = 0;
+  void* stream_ = nullptr;
+  std::string err_;
+  bool have_mask_scale_ = false;
+
+  // device buffers
+  uint8_t* d_rgb_ = nullptr;
+  int16_t* d_orig_ = nullptr;
+  int16_t* d_cur_ = nullptr;
+  float* d_ref_xyb_ = nullptr;
+  float* d_lin_ = nullptr;
+  float* d_xyb_ = nullptr;
+  float* d_m0_ = nullptr;
+  float* d_m1_ = nullptr;
+  float* d_tmp_ = nullptr;   // 6 planes
+  float* d_bl_ = nullptr;    // 6 planes
+  float* d_ma_ = nullptr;    // 3 planes
+  float* d_mb_ = nullptr;    // 3 planes
+  float* d_edge_ = nullptr;  // 3R
+  float* d_dc_ = nullptr;    // 3R
+  float* d_ac_ = nullptr;    // 3R
+  float* d_resval_ = nullptr;
+  float* d_dd_ = nullptr;
+  float* d_block_max_ = nullptr;
+  unsigned* d_gmax_ = nullptr;
+  float* d_mask_scale_ = nullptr;
+  void* d_zero_out_ = nullptr;
+  // pinned host staging
+  unsigned* h_gmax_ = nullptr;
+};
+
+// Version / build string of the device library.
+const char* BuildInfo();
+
+}  // namespace gz

@@ -1,0 +1,154 @@
+/*
+ * guetzli_hip.h — C ABI of the MI355X-native Guetzli search path
+ * (libguetzli_hip.so, built from guetzli-cuda-opencl_amd/csrc).
+ *
+ * Drop-in boundary for the reference's hot path (yyamamoto79/guetzli-cuda-
+ * opencl): the library-level encode call `guetzli::Process`
+ * (guetzli/processor.h:62-64) and the comparator that the search loop talks
+ * to (`guetzli::Comparator`, guetzli/comparator.h:29-96, implemented by
+ * `guetzli::ButteraugliComparator`, guetzli/butteraugli_comparator.h:33-81),
+ * plus the batched per-block zeroing entry of the reference GPU fast path
+ * (`cuComputeBlockZeroingOrder`, clguetzli/cuguetzli.h:30-40).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every call returns gz_status; on failure
+ *    gz_last_error() (thread-local) describes it.  No call silently falls
+ *    back to the CPU: without a usable HIP device they fail with
+ *    GZ_ERR_DEVICE.
+ *  - Images: 8-bit RGB, interleaved, row-major, no padding (3*w*h bytes).
+ *  - Coefficients: int16, [3][blocks][64], natural (row-major) order inside
+ *    a block, blocks row-major with ceil(w/8) blocks per row (the layout of
+ *    guetzli::JPEGComponent::coeffs, guetzli/jpeg_data.h:138-204).
+ *  - One gz_comparator / gz_encoder owns one HIP stream and its device
+ *    buffers; distinct objects may be used from distinct host threads.
+ */
+#ifndef GUETZLI_HIP_H_
+#define GUETZLI_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int gz_status;
+enum {
+  GZ_OK = 0,
+  GZ_ERR_INVALID_ARG = 1,
+  GZ_ERR_DEVICE = 2,
+  GZ_ERR_OUT_OF_MEMORY = 3,
+  GZ_ERR_UNSUPPORTED = 4,
+  GZ_ERR_INTERNAL = 5,
+};
+
+/* guetzli::CoeffData (guetzli/processor.h:29-32). */
+typedef struct {
+  int idx;
+  float block_err;
+} gz_coeff_data;
+
+/* guetzli::Params (guetzli/processor.h:34-42); same defaults via
+ * gz_params_init().  try_420 / force_420 are not supported (GZ_ERR_UNSUPPORTED). */
+typedef struct {
+  float butteraugli_target;
+  int clear_metadata;
+  int try_420;
+  int force_420;
+  int use_silver_screen;
+  int zeroing_greedy_lookahead;
+  int new_zeroing_model;
+} gz_params;
+
+/* guetzli::ProcessStats counters (guetzli/stats.h:26-41). */
+typedef struct {
+  int iterations;        /* "number of iterations" */
+  int iterations_up;     /* "number of iterations up" */
+  int iterations_down;   /* "number of iterations down" */
+  int compares;          /* full-image Butteraugli passes */
+  double seconds_compare;   /* wall time inside Compare calls */
+  double seconds_zeroing;   /* wall time of the per-block search */
+  double seconds_total;
+} gz_process_stats;
+
+/* Stage dumps of one compare (parity tests); any pointer may be NULL.
+ * Plane arrays are 3*w*h floats, res arrays 3*ceil(w/3)*ceil(h/3). */
+typedef struct {
+  float* cand_linear;
+  float* cand_xyb;
+  float* mhic0;
+  float* mhic1;
+  float* edge;
+  float* block_dc;
+  float* block_ac;
+  float* block_ac_lf;
+  float* mask;
+  float* mask_dc;
+  float* combined;   /* ceil(w/3)*ceil(h/3) */
+  float* distmap;    /* w*h */
+} gz_compare_stages;
+
+typedef struct gz_comparator gz_comparator;
+
+/* ---- library ---------------------------------------------------------- */
+const char* gz_last_error(void);
+const char* gz_build_info(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int gz_device_count(void);
+void gz_params_init(gz_params* params);
+/* guetzli::ButteraugliScoreForQuality (guetzli/quality.cc:78-87). */
+double gz_butteraugli_score_for_quality(double quality);
+void gz_free(void* p);
+
+/* ---- encode (guetzli::Process, guetzli/processor.h:62-64) -------------- */
+/* Encodes an RGB image; *jpeg_out is allocated by the library (gz_free). */
+gz_status gz_process_rgb(int device, const gz_params* params, const uint8_t* rgb, int width,
+                         int height, uint8_t** jpeg_out, size_t* jpeg_size,
+                         gz_process_stats* stats);
+/* Same, with the RGB image already resident on `device` (HBM pointer). */
+gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8_t* rgb_dev,
+                                int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
+                                gz_process_stats* stats);
+
+/* ---- comparator (guetzli::ButteraugliComparator) ---------------------- */
+/* ButteraugliComparator(w, h, rgb, target, stats) ctor
+ * (guetzli/butteraugli_comparator.cc:48-58); width, height >= 8. */
+gz_status gz_comparator_create(int device, int width, int height, const uint8_t* rgb,
+                               float target_distance, gz_comparator** out);
+void gz_comparator_destroy(gz_comparator* cmp);
+/* Comparator::Compare (guetzli/butteraugli_comparator.cc:60-70) on the image
+ * whose DCT coefficients are `coeffs`; distance = distmap_aggregate(). */
+gz_status gz_comparator_compare(gz_comparator* cmp, const int16_t* coeffs, float* distance);
+/* Same, with stage dumps. */
+gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs,
+                                       gz_compare_stages* stages, float* distance);
+/* Per-8x8-block maxima of the last distance map (ceil(w/8)*ceil(h/8)). */
+gz_status gz_comparator_block_max(gz_comparator* cmp, float* out);
+/* Comparator::DistanceOK (butteraugli_comparator.h:52-54). */
+int gz_comparator_distance_ok(gz_comparator* cmp, double target_mul);
+/* Comparator::ScoreOutputSize (butteraugli_comparator.cc:235-237). */
+double gz_comparator_score_output_size(gz_comparator* cmp, int size);
+/* StartBlockComparisons (butteraugli_comparator.cc:72-79); mask_scale may be
+ * NULL, else receives 3 floats per block (mask_xyz at the block corner). */
+gz_status gz_comparator_start_block_comparisons(gz_comparator* cmp, float* mask_scale);
+/* Batched per-block greedy zeroing of SelectFrequencyMasking's CPU_OPT loop
+ * (processor.cc:376-487, 641-672) for the candidate `cur_coeffs` against
+ * the original q=1 coefficients `orig_coeffs`; out: blocks*192 entries,
+ * zero-filled tails.  Replaces cuComputeBlockZeroingOrder
+ * (clguetzli/cuguetzli.h:30-40). */
+gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* cur_coeffs,
+                                             const int16_t* orig_coeffs, int comp_mask,
+                                             float limit, int lookahead, gz_coeff_data* out);
+
+/* ---- helpers used by the host search loop ----------------------------- */
+/* Synthetic sRGB test frame (SURVEY.md §8d generator), 3*w*h bytes. */
+gz_status gz_synthetic_frame(uint64_t seed, int width, int height, uint8_t* rgb_out);
+/* EncodeRGBToJpeg at q=1 (guetzli/jpeg_data_encoder.cc:66-136): coefficient
+ * planes [3][blocks][64]. */
+gz_status gz_rgb_to_coeffs(const uint8_t* rgb, int width, int height, int16_t* coeffs_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GUETZLI_HIP_H_ */
