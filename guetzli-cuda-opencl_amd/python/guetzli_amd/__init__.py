@@ -1,0 +1,319 @@
+"""Python host mirror of the reference's encode / comparator API.
+
+Thin ctypes layer over the C ABI in include/guetzli_hip.h (libguetzli_hip.so,
+built from guetzli-cuda-opencl_amd/csrc).  Names follow the reference:
+
+  process(rgb, w, h, params)        guetzli::Process          processor.h:62-64
+  Params                            guetzli::Params           processor.h:34-42
+  butteraugli_score_for_quality(q)  ButteraugliScoreForQuality quality.cc:78-87
+  ButteraugliComparator             guetzli::ButteraugliComparator
+                                    butteraugli_comparator.h:33-81
+
+There is no CPU fallback: every compute call goes through the HIP library and
+raises GuetzliError when the library or a GPU is unavailable.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libguetzli_hip.so")
+
+GZ_OK = 0
+_STATUS = {1: "invalid argument", 2: "device error", 3: "out of memory", 4: "unsupported",
+           5: "internal error"}
+
+
+class GuetzliError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("%s (%s)" % (message, _STATUS.get(status, status)))
+        self.status = status
+
+
+class _CoeffData(ctypes.Structure):
+    _fields_ = [("idx", ctypes.c_int), ("block_err", ctypes.c_float)]
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("butteraugli_target", ctypes.c_float), ("clear_metadata", ctypes.c_int),
+                ("try_420", ctypes.c_int), ("force_420", ctypes.c_int),
+                ("use_silver_screen", ctypes.c_int), ("zeroing_greedy_lookahead", ctypes.c_int),
+                ("new_zeroing_model", ctypes.c_int)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int), ("iterations_up", ctypes.c_int),
+                ("iterations_down", ctypes.c_int), ("compares", ctypes.c_int),
+                ("seconds_compare", ctypes.c_double), ("seconds_zeroing", ctypes.c_double),
+                ("seconds_total", ctypes.c_double)]
+
+
+_STAGE_FIELDS = ("cand_linear", "cand_xyb", "mhic0", "mhic1", "edge", "block_dc", "block_ac",
+                 "block_ac_lf", "mask", "mask_dc", "combined", "distmap")
+
+
+class _Stages(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in _STAGE_FIELDS]
+
+
+COEFF_DTYPE = np.dtype([("idx", "<i4"), ("block_err", "<f4")])
+
+# Every symbol include/guetzli_hip.h declares.
+EXPORTED_SYMBOLS = (
+    "gz_last_error", "gz_build_info", "gz_device_count", "gz_params_init",
+    "gz_butteraugli_score_for_quality", "gz_free", "gz_process_rgb", "gz_process_rgb_device",
+    "gz_comparator_create", "gz_comparator_destroy", "gz_comparator_compare",
+    "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
+    "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
+    "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libguetzli_hip.so (raises GuetzliError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GuetzliError(2, "libguetzli_hip.so not built at %s (run __graft_entry__.build())"
+                           % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, f32, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
+    L.gz_last_error.restype = ctypes.c_char_p
+    L.gz_build_info.restype = ctypes.c_char_p
+    L.gz_device_count.restype = i32
+    L.gz_params_init.argtypes = [ctypes.POINTER(_Params)]
+    L.gz_butteraugli_score_for_quality.argtypes = [ctypes.c_double]
+    L.gz_butteraugli_score_for_quality.restype = ctypes.c_double
+    L.gz_free.argtypes = [vp]
+    for name in ("gz_process_rgb", "gz_process_rgb_device"):
+        fn = getattr(L, name)
+        fn.argtypes = [i32, ctypes.POINTER(_Params), vp, i32, i32, ctypes.POINTER(vp),
+                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_Stats)]
+        fn.restype = i32
+    L.gz_comparator_create.argtypes = [i32, i32, i32, vp, f32, ctypes.POINTER(vp)]
+    L.gz_comparator_create.restype = i32
+    L.gz_comparator_destroy.argtypes = [vp]
+    L.gz_comparator_compare.argtypes = [vp, vp, ctypes.POINTER(f32)]
+    L.gz_comparator_compare.restype = i32
+    L.gz_comparator_compare_stages.argtypes = [vp, vp, ctypes.POINTER(_Stages), ctypes.POINTER(f32)]
+    L.gz_comparator_compare_stages.restype = i32
+    L.gz_comparator_block_max.argtypes = [vp, vp]
+    L.gz_comparator_block_max.restype = i32
+    L.gz_comparator_distance_ok.argtypes = [vp, ctypes.c_double]
+    L.gz_comparator_distance_ok.restype = i32
+    L.gz_comparator_score_output_size.argtypes = [vp, i32]
+    L.gz_comparator_score_output_size.restype = ctypes.c_double
+    L.gz_comparator_start_block_comparisons.argtypes = [vp, vp]
+    L.gz_comparator_start_block_comparisons.restype = i32
+    L.gz_comparator_block_zeroing_orders.argtypes = [vp, vp, vp, i32, f32, i32, vp]
+    L.gz_comparator_block_zeroing_orders.restype = i32
+    L.gz_synthetic_frame.argtypes = [u64, i32, i32, vp]
+    L.gz_synthetic_frame.restype = i32
+    L.gz_rgb_to_coeffs.argtypes = [vp, i32, i32, vp]
+    L.gz_rgb_to_coeffs.restype = i32
+    _lib = L
+    return L
+
+
+def _check(status, what):
+    if status != GZ_OK:
+        raise GuetzliError(status, "%s: %s" % (what, lib().gz_last_error().decode()))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    return lib().gz_device_count()
+
+
+def build_info():
+    return lib().gz_build_info().decode()
+
+
+def butteraugli_score_for_quality(quality):
+    return lib().gz_butteraugli_score_for_quality(float(quality))
+
+
+@dataclass
+class Params:
+    """guetzli::Params (processor.h:34-42)."""
+    butteraugli_target: float = 1.0
+    clear_metadata: bool = True
+    try_420: bool = False
+    force_420: bool = False
+    use_silver_screen: bool = False
+    zeroing_greedy_lookahead: int = 3
+    new_zeroing_model: bool = True
+
+    @classmethod
+    def for_quality(cls, quality, **kw):
+        # guetzli.cc:312-314: target = float(ButteraugliScoreForQuality(quality))
+        t = float(np.float32(butteraugli_score_for_quality(quality)))
+        return cls(butteraugli_target=t, **kw)
+
+    def _c(self):
+        return _Params(self.butteraugli_target, int(self.clear_metadata), int(self.try_420),
+                       int(self.force_420), int(self.use_silver_screen),
+                       int(self.zeroing_greedy_lookahead), int(self.new_zeroing_model))
+
+
+@dataclass
+class ProcessStats:
+    iterations: int
+    iterations_up: int
+    iterations_down: int
+    compares: int
+    seconds_compare: float
+    seconds_zeroing: float
+    seconds_total: float
+
+
+def _as_rgb(rgb, width, height):
+    a = np.ascontiguousarray(np.frombuffer(rgb, dtype=np.uint8) if isinstance(rgb, (bytes, bytearray))
+                             else np.asarray(rgb, dtype=np.uint8)).reshape(-1)
+    if a.size != 3 * width * height:
+        raise GuetzliError(1, "rgb has %d bytes, expected %d" % (a.size, 3 * width * height))
+    return a
+
+
+def process(rgb, width, height, params=None, device=0, return_stats=False):
+    """guetzli::Process on an RGB8 image -> JPEG bytes (bit-identical to `guetzli --c`)."""
+    L = lib()
+    a = _as_rgb(rgb, width, height)
+    p = (params or Params())._c()
+    out = ctypes.c_void_p()
+    size = ctypes.c_size_t()
+    st = _Stats()
+    _check(L.gz_process_rgb(device, ctypes.byref(p), _ptr(a), width, height, ctypes.byref(out),
+                            ctypes.byref(size), ctypes.byref(st)), "process")
+    data = ctypes.string_at(out, size.value)
+    L.gz_free(out)
+    if return_stats:
+        return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
+                                  st.compares, st.seconds_compare, st.seconds_zeroing,
+                                  st.seconds_total)
+    return data
+
+
+def process_device(rgb_dev_ptr, width, height, params=None, device=0, return_stats=False):
+    """Same as process() with the RGB image already resident in HBM (device pointer)."""
+    L = lib()
+    p = (params or Params())._c()
+    out = ctypes.c_void_p()
+    size = ctypes.c_size_t()
+    st = _Stats()
+    _check(L.gz_process_rgb_device(device, ctypes.byref(p), ctypes.c_void_p(rgb_dev_ptr), width,
+                                   height, ctypes.byref(out), ctypes.byref(size),
+                                   ctypes.byref(st)), "process_device")
+    data = ctypes.string_at(out, size.value)
+    L.gz_free(out)
+    if return_stats:
+        return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
+                                  st.compares, st.seconds_compare, st.seconds_zeroing,
+                                  st.seconds_total)
+    return data
+
+
+def synthetic_frame(seed, width, height):
+    """Deterministic synthetic sRGB frame, shape (h, w, 3) uint8."""
+    out = np.zeros(3 * width * height, dtype=np.uint8)
+    _check(lib().gz_synthetic_frame(seed, width, height, _ptr(out)), "synthetic_frame")
+    return out.reshape(height, width, 3)
+
+
+def rgb_to_coeffs(rgb, width, height):
+    """q=1 DCT coefficients of an RGB image, [3][blocks][64] int16."""
+    a = _as_rgb(rgb, width, height)
+    nb = ((width + 7) // 8) * ((height + 7) // 8)
+    out = np.zeros(3 * nb * 64, dtype=np.int16)
+    _check(lib().gz_rgb_to_coeffs(_ptr(a), width, height, _ptr(out)), "rgb_to_coeffs")
+    return out
+
+
+class ButteraugliComparator:
+    """guetzli::ButteraugliComparator (butteraugli_comparator.h:33-81) on the GPU."""
+
+    def __init__(self, width, height, rgb, target_distance, device=0):
+        L = lib()
+        self.width, self.height = width, height
+        self.blocks = ((width + 7) // 8) * ((height + 7) // 8)
+        self._rgb = _as_rgb(rgb, width, height)
+        h = ctypes.c_void_p()
+        _check(L.gz_comparator_create(device, width, height, _ptr(self._rgb),
+                                      ctypes.c_float(target_distance), ctypes.byref(h)),
+               "comparator_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().gz_comparator_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _coeffs(self, coeffs):
+        c = np.ascontiguousarray(coeffs, dtype=np.int16).reshape(-1)
+        if c.size != 3 * self.blocks * 64:
+            raise GuetzliError(1, "coefficient array has %d entries, expected %d"
+                               % (c.size, 3 * self.blocks * 64))
+        return c
+
+    def compare(self, coeffs):
+        """Comparator::Compare; returns distmap_aggregate()."""
+        d = ctypes.c_float()
+        _check(lib().gz_comparator_compare(self._h, _ptr(self._coeffs(coeffs)), ctypes.byref(d)),
+               "compare")
+        return d.value
+
+    def compare_stages(self, coeffs):
+        """Compare with every intermediate stage returned (parity tests)."""
+        n = self.width * self.height
+        rn = ((self.width + 2) // 3) * ((self.height + 2) // 3)
+        sizes = {"cand_linear": 3 * n, "cand_xyb": 3 * n, "mhic0": 3 * n, "mhic1": 3 * n,
+                 "edge": 3 * rn, "block_dc": 3 * rn, "block_ac": 3 * rn, "block_ac_lf": 3 * rn,
+                 "mask": 3 * n, "mask_dc": 3 * n, "combined": rn, "distmap": n}
+        arrs = {k: np.zeros(v, dtype=np.float32) for k, v in sizes.items()}
+        st = _Stages(**{k: a.ctypes.data for k, a in arrs.items()})
+        d = ctypes.c_float()
+        _check(lib().gz_comparator_compare_stages(self._h, _ptr(self._coeffs(coeffs)),
+                                                  ctypes.byref(st), ctypes.byref(d)),
+               "compare_stages")
+        arrs["distance"] = d.value
+        return arrs
+
+    def block_max(self):
+        out = np.zeros(self.blocks, dtype=np.float32)
+        _check(lib().gz_comparator_block_max(self._h, _ptr(out)), "block_max")
+        return out
+
+    def distance_ok(self, target_mul):
+        return bool(lib().gz_comparator_distance_ok(self._h, float(target_mul)))
+
+    def score_output_size(self, size):
+        return lib().gz_comparator_score_output_size(self._h, int(size))
+
+    def start_block_comparisons(self):
+        out = np.zeros(3 * self.blocks, dtype=np.float32)
+        _check(lib().gz_comparator_start_block_comparisons(self._h, _ptr(out)),
+               "start_block_comparisons")
+        return out.reshape(self.blocks, 3)
+
+    def block_zeroing_orders(self, cur_coeffs, orig_coeffs, limit, comp_mask=7, lookahead=3):
+        out = np.zeros(self.blocks * 192, dtype=COEFF_DTYPE)
+        _check(lib().gz_comparator_block_zeroing_orders(
+            self._h, _ptr(self._coeffs(cur_coeffs)), _ptr(self._coeffs(orig_coeffs)), comp_mask,
+            ctypes.c_float(limit), lookahead, ctypes.c_void_p(out.ctypes.data)),
+            "block_zeroing_orders")
+        return out.reshape(self.blocks, 192)

@@ -1,0 +1,57 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: long-running CPU oracle comparison")
+
+
+def _ensure_built():
+    lib = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib", "libguetzli_hip.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
+                        "-j8"], check=True, stdout=subprocess.DEVNULL)
+    oracle = os.path.join(ROOT, "oracle", "_build", "libgz_oracle.so")
+    if not os.path.exists(oracle):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], check=True,
+                       stdout=subprocess.DEVNULL)
+
+
+_ensure_built()
+
+
+@pytest.fixture(scope="session")
+def gz():
+    import guetzli_amd
+    return guetzli_amd
+
+
+@pytest.fixture(scope="session")
+def gpu_available(gz):
+    return gz.device_count() > 0
+
+
+@pytest.fixture(scope="session")
+def host_e2e_bin():
+    """tests/native/host_oracle_e2e: product host loop + CPU-oracle comparator."""
+    out = os.path.join(ROOT, "tests", "_build", "host_oracle_e2e")
+    src = os.path.join(ROOT, "tests", "native", "host_oracle_e2e.cc")
+    lib_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib")
+    oracle_dir = os.path.join(ROOT, "oracle", "_build")
+    if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+                        "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
+                        "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+                        src, "-o", out, "-L", lib_dir, "-lguetzli_hip", "-L", oracle_dir,
+                        "-lgz_oracle", "-Wl,-rpath," + lib_dir, "-Wl,-rpath," + oracle_dir],
+                       check=True)
+    return out

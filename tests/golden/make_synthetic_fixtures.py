@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Known answers of the reference (`guetzli --c`, oracle/_ref) on synthetic
+frames from the product's deterministic generator (gz_synthetic_frame).
+Build container only; writes tests/golden/manifest.json["synthetic"].
+
+  python tests/golden/make_synthetic_fixtures.py [name ...]
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+import guetzli_amd  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "guetzli_ref")
+CASES = {
+    "synth_256x256_s0_q95": (0, 256, 256, 95),
+    "synth_640x360_s3_q95": (3, 640, 360, 95),
+    "synth_1920x1080_s0_q95": (0, 1920, 1080, 95),
+    "synth_1920x1080_s1_q95": (1, 1920, 1080, 95),
+    "synth_3840x2160_s0_q90": (0, 3840, 2160, 90),
+}
+
+
+def main():
+    names = sys.argv[1:] or list(CASES)
+    path = os.path.join(HERE, "manifest.json")
+    for name in names:
+        seed, w, h, q = CASES[name]
+        rgb = guetzli_amd.synthetic_frame(seed, w, h).tobytes()
+        inp = "/tmp/gz_%s.rgb" % name
+        open(inp, "wb").write(rgb)
+        jpg = "/tmp/gz_%s.jpg" % name
+        res = subprocess.run([REF, "encode", inp, str(w), str(h), str(q), jpg, "c"], check=True,
+                             capture_output=True, text=True)
+        info = json.loads(res.stdout)
+        manifest = json.load(open(path))
+        manifest.setdefault("synthetic", {})[name] = {
+            "seed": seed, "w": w, "h": h, "quality": q,
+            "input_sha256": hashlib.sha256(rgb).hexdigest(),
+            "sha256": hashlib.sha256(open(jpg, "rb").read()).hexdigest(),
+            "bytes": info["bytes"], "iters": info["iters"], "ref_seconds": info["seconds"]}
+        json.dump(manifest, open(path, "w"), indent=1, sort_keys=True)
+        print(name, manifest["synthetic"][name], flush=True)
+
+
+if __name__ == "__main__":
+    main()

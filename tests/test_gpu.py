@@ -1,0 +1,132 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference.
+
+Bit-exact against fixtures produced by the reference itself (oracle/_ref):
+every stage of one Butteraugli pass, the block-corner activity mask, the
+per-block greedy zeroing orders, and end-to-end JPEG bytes (sha256) of
+`guetzli --c` on bees.png and synthetic frames.  Larger frames are checked
+against the CPU oracle at sizes it finishes in seconds.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle_lib import COEFF_DTYPE, GOLDEN, Fixture, fixture_cases, lib as oracle
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+STAGES = ["cand_linear", "cand_xyb", "mhic0", "mhic1", "edge", "block_dc", "block_ac",
+          "block_ac_lf", "mask", "mask_dc", "combined", "distmap"]
+FIXTURE_FILE = {"block_dc": "block_dc.f32", "block_ac": "block_ac.f32",
+                "block_ac_lf": "block_ac_lf.f32", "distmap": "distmap.f32"}
+
+
+def bits_equal(a, b):
+    a = np.asarray(a, dtype=np.float32).ravel()
+    b = np.asarray(b, dtype=np.float32).ravel()
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def mismatch(a, b):
+    a = np.asarray(a, dtype=np.float32).ravel()
+    b = np.asarray(b, dtype=np.float32).ravel()
+    bad = a.view(np.uint32) != b.view(np.uint32)
+    return "%d/%d differ, max |d| %.3g" % (bad.sum(), bad.size,
+                                          np.max(np.abs(a.astype(np.float64) - b)) if bad.any() else 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu(gz):
+    if gz.device_count() == 0:
+        pytest.fail("no HIP device visible: -m gpu tests need an MI355X")
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_compare_stages_bit_exact(gz, case):
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    st = cmp.compare_stages(F.i16("cand_coeffs.i16"))
+    bad = []
+    for name in STAGES:
+        ref = F.f32(FIXTURE_FILE.get(name, name + ".f32"))
+        if not bits_equal(st[name], ref):
+            bad.append("%s: %s" % (name, mismatch(st[name], ref)))
+    assert not bad, "; ".join(bad)
+    assert np.float32(st["distance"]) == np.float32(F.meta["distance"])
+    # per-block maxima of the distance map (ComputeBlockErrorAdjustmentWeights input)
+    dm = F.f32("distmap.f32").reshape(F.h, F.w)
+    bm = np.zeros(F.nb, np.float32)
+    for by in range(F.bh):
+        for bx in range(F.bw):
+            bm[by * F.bw + bx] = max(0.0, dm[8 * by:8 * by + 8, 8 * bx:8 * bx + 8].max())
+    assert bits_equal(cmp.block_max(), bm)
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_block_mask_scale_bit_exact(gz, case):
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    scale = cmp.start_block_comparisons()
+    m = F.planes("ref_mask.f32")
+    exp = np.stack([m[:, 8 * (b // F.bw), 8 * (b % F.bw)] for b in range(F.nb)])
+    assert bits_equal(scale, exp)
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_block_zeroing_orders_bit_exact(gz, case):
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    out = cmp.block_zeroing_orders(F.i16("cand_coeffs.i16"), F.i16("orig_coeffs.i16"), F.target)
+    z = F.zero_order()
+    assert np.array_equal(out["idx"], z["idx"]), "idx differ in %d blocks" % (
+        (out["idx"] != z["idx"]).any(axis=1).sum())
+    assert bits_equal(out["block_err"], z["block_err"]), mismatch(out["block_err"], z["block_err"])
+
+
+def _jpeg_sha(gz, rgb, w, h, q):
+    data, stats = gz.process(rgb, w, h, gz.Params.for_quality(q), return_stats=True)
+    return hashlib.sha256(data).hexdigest(), stats
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST["e2e"]))
+def test_process_reference_known_answers(gz, name):
+    e = MANIFEST["e2e"][name]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    sha, stats = _jpeg_sha(gz, rgb, e["w"], e["h"], e["quality"])
+    assert stats.iterations == e["iters"]
+    assert sha == e["sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST.get("synthetic", {})))
+def test_process_synthetic_known_answers(gz, name):
+    e = MANIFEST["synthetic"][name]
+    rgb = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == e["input_sha256"]
+    sha, stats = _jpeg_sha(gz, rgb, e["w"], e["h"], e["quality"])
+    assert stats.iterations == e["iters"]
+    assert sha == e["sha256"]
+
+
+@pytest.mark.parametrize("w,h,seed", [(256, 256, 7), (333, 197, 8)])
+def test_compare_matches_oracle_on_synthetic(gz, w, h, seed):
+    """Full-pass distance map vs the CPU oracle on frames it finishes in ~1 s."""
+    L = oracle()
+    rgb = gz.synthetic_frame(seed, w, h)
+    coeffs = gz.rgb_to_coeffs(rgb, w, h)
+    rng = np.random.default_rng(seed)
+    q = rng.integers(1, 12, size=(3, 64))
+    nb = ((w + 7) // 8) * ((h + 7) // 8)
+    c = coeffs.reshape(3, nb, 64).astype(np.int32)
+    qq = q[:, None, :]
+    r = np.fmod(c, qq)
+    delta = np.where(2 * r > qq, qq - r, np.where(-2 * r > qq, -qq - r, -r))
+    cand = (c + delta).astype(np.int16).ravel()
+    cmp = gz.ButteraugliComparator(w, h, rgb, 1.0)
+    st = cmp.compare_stages(cand)
+    dm = np.zeros(w * h, np.float32)
+    d = L.gzo_compare(w, h, rgb.ravel(), cand, dm)
+    assert bits_equal(st["distmap"], dm), mismatch(st["distmap"], dm)
+    assert np.float32(st["distance"]) == np.float32(d)

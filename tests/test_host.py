@@ -1,0 +1,108 @@
+"""Host-side checks that need no GPU.
+
+- the C-ABI library loads and exports every symbol include/guetzli_hip.h
+  declares (no compute calls);
+- the product's initial encoder (EncodeRGBToJpeg: RGB->YUV16 + integer FDCT,
+  q=1) reproduces the reference's coefficients;
+- the product's host search loop, quantizer and JPEG writer, driven by the
+  CPU oracle as comparator (tests/native/host_oracle_e2e.cc), reproduce the
+  reference's output bytes end to end;
+- the synthetic frame generator is deterministic;
+- without a GPU the compute entry points fail loudly (no CPU fallback).
+"""
+import hashlib
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle_lib import GOLDEN, Fixture, fixture_cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "guetzli_hip.h")).read()
+    return sorted(set(re.findall(r"\b(gz_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(gz):
+    L = gz.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    assert sorted(gz.EXPORTED_SYMBOLS) == syms
+    for s in syms:
+        assert hasattr(L, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", gz.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if line.strip())
+    for s in syms:
+        assert s in exported, s
+
+
+def test_quality_to_target(gz):
+    # guetzli/quality.cc:46-57
+    assert gz.butteraugli_score_for_quality(95) == pytest.approx(0.971769, abs=0)
+    assert gz.butteraugli_score_for_quality(90) == pytest.approx(1.473608, abs=0)
+    assert gz.butteraugli_score_for_quality(84) == pytest.approx(1.945456, abs=0)
+    assert gz.butteraugli_score_for_quality(50) == pytest.approx(2.810761, abs=0)
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_rgb_to_coeffs_matches_reference(gz, case):
+    F = Fixture(case)
+    c = gz.rgb_to_coeffs(F.rgb(), F.w, F.h)
+    assert np.array_equal(c, F.i16("orig_coeffs.i16"))
+
+
+def _e2e_cases():
+    cases = []
+    for name, e in sorted(MANIFEST["e2e"].items()):
+        if e["w"] * e["h"] <= 100 * 100 or name == "bees_q95":
+            cases.append(name)
+    return cases
+
+
+@pytest.mark.parametrize("name", _e2e_cases())
+def test_host_loop_with_oracle_comparator_bit_exact(host_e2e_bin, name, tmp_path):
+    e = MANIFEST["e2e"][name]
+    out = tmp_path / "out.jpg"
+    res = subprocess.run([host_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]), str(e["h"]),
+                          str(e["quality"]), str(out)], capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr
+    info = json.loads(res.stdout)
+    assert info["iters"] == e["iters"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+
+
+def test_synthetic_frames_deterministic(gz):
+    for name, e in MANIFEST.get("synthetic", {}).items():
+        if e["w"] * e["h"] > 640 * 360:
+            continue
+        f = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+        assert f.shape == (e["h"], e["w"], 3)
+        assert hashlib.sha256(f.tobytes()).hexdigest() == e["input_sha256"], name
+        assert f.min() >= 16 and f.max() <= 240
+
+
+def test_bad_arguments_fail_loudly(gz):
+    with pytest.raises(gz.GuetzliError):
+        gz.rgb_to_coeffs(np.zeros(10, np.uint8), 4, 4)
+    with pytest.raises(gz.GuetzliError):
+        gz.process(np.zeros(3 * 64 * 64, np.uint8), 64, 64, gz.Params(try_420=True))
+
+
+def test_no_cpu_fallback_without_gpu(gz, gpu_available):
+    if gpu_available:
+        pytest.skip("a GPU is present")
+    rgb = np.zeros(3 * 64 * 64, np.uint8)
+    with pytest.raises(gz.GuetzliError) as e:
+        gz.ButteraugliComparator(64, 64, rgb, 1.0)
+    assert e.value.status == 2
+    with pytest.raises(gz.GuetzliError) as e:
+        gz.process(rgb, 64, 64, gz.Params.for_quality(95))
+    assert e.value.status == 2
