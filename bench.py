@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Guetzli search path (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step is one end-to-end `guetzli::Process` encode per GPU of a synthetic
+sRGB frame (BASELINE.json configs[1]: 1920x1080, q=95), with the input frame
+already resident in HBM when the timed region starts.  For N > 1 (launched by
+torch.distributed.run, one rank per GPU) every rank encodes its own frames
+(image-level sharding, no data-path collective) and the JPEG byte strings
+are gathered to rank 0 over RCCL at the end of each step (BASELINE configs[3]
+pattern).  value = total pixels of all ranks / max-over-ranks wall time.
+
+Also reported (one JSON line on rank 0):
+  roofline      dominant HBM-bound kernel of the Butteraugli pass, timed with
+                HIP events on the engine's own stream inside the library
+                (gz_profile_*), against algorithmic bytes per launch.
+  cpu_baseline  the reference `guetzli --c` (oracle/_ref, built from the
+                reference sources) on the host cores, on a bounded sample.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+
+METRIC = "Mpixels/s end-to-end encode @ q=95; achieved HBM GB/s on Butteraugli pass"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# Algorithmic HBM bytes per pixel of each Compare-pass kernel: every input
+# plane read once and every output plane written once (f32 = 4 B; res-grid
+# arrays at 1/9 of a plane; blur h passes write a 1/step-wide plane, v passes
+# read it and write 1/step^2).  Derivation in DESIGN.md §4.
+def stage_bytes_per_px():
+    s = {}
+    s["coeffs_to_linear"] = 3 * 2 + 3 * 4          # int16 coeffs -> 3 f32 planes
+    s["opsin_blur_h"] = 3 * 4 + 3 * 4
+    s["opsin_v"] = 3 * 4 + 3 * 4 + 3 * 4           # tmp + linear -> xyb
+    s["mhic"] = 6 * 4 + 6 * 4
+    s["edge_blur_h"] = 6 * 4 + 6 * 4
+    s["edge_blur_v"] = 6 * 4 + 6 * 4
+    s["edge_map"] = 6 * 4 + 3 * 4 / 9.0
+    s["block_diff"] = 6 * 4 + 6 * 4 / 9.0
+    s["lowfreq_blur_h"] = 6 * 4 + 6 * 4 / 4.0
+    s["lowfreq_blur_v"] = 6 * 4 / 4.0 + 6 * 4 / 16.0
+    s["low_freq"] = 6 * 4 / 16.0 + 2 * 3 * 4 / 9.0
+    s["mask_diff_precompute"] = 6 * 4 + 3 * 4
+    s["mask_average5x5"] = 3 * 4 + 3 * 4
+    s["mask_min4_v"] = 3 * 4 + 3 * 4
+    s["mask_min4_h"] = 3 * 4 + 3 * 4
+    s["mask_blur_h"] = 3 * 4 + 4 * (1 / 3.0 + 1 / 4.0 + 1.0)
+    s["mask_blur_v"] = 4 * (1 / 3.0 + 1 / 4.0 + 1.0) + 4 * (1 / 9.0 + 1 / 16.0 + 1.0)
+    s["combine"] = (3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 4) / 9.0
+    s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
+    s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
+    s["diffmap_final"] = 4 / 9.0 + 4 / 4.0 + 4 / 64.0
+    return s
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist
+
+
+def cpu_baseline(width, height, quality, seconds_budget=25.0):
+    """Reference `guetzli --c` (oracle/_ref) on host cores: concurrent single-
+    threaded processes on distinct synthetic frames of the workload's kind,
+    scaled down so the sample is ~10-30 s of CPU work."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "guetzli_ref")
+    if not os.path.exists(ref):
+        return {"value": None, "unit": "Mpixels/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/guetzli_ref not built"}
+    import guetzli_amd as gz
+    cores = max(1, min(8, len(os.sched_getaffinity(0))))
+    # ~24.5 us/px single-threaded (survey: 1080p in 47-51 s); size the frame so
+    # each process runs ~seconds_budget / cores ... capped to a quarter frame.
+    sw, sh = width // 2, height // 2
+    tmp = tempfile.mkdtemp(prefix="gz_cpu_")
+    procs = []
+    t0 = time.time()
+    for i in range(cores):
+        rgb = gz.synthetic_frame(1000 + i, sw, sh)
+        path = os.path.join(tmp, "f%d.rgb" % i)
+        rgb.tofile(path)
+        procs.append(subprocess.Popen([ref, "encode", path, str(sw), str(sh), str(quality),
+                                       os.path.join(tmp, "f%d.jpg" % i), "c"],
+                                      stdout=subprocess.PIPE, stderr=subprocess.DEVNULL))
+    outs = [json.loads(p.communicate()[0]) for p in procs]
+    wall = time.time() - t0
+    px = cores * sw * sh
+    return {"value": px / wall / 1e6, "unit": "Mpixels/s", "cores": cores, "kind": "reference",
+            "sample": "%d concurrent single-threaded `guetzli --c` processes, one synthetic "
+                      "%dx%d q%d frame each (seeds 1000..%d), %.1f s wall, %.1f s CPU" % (
+                          cores, sw, sh, quality, 999 + cores, wall,
+                          sum(o["seconds"] for o in outs)),
+            "per_process_seconds": [round(o["seconds"], 2) for o in outs]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--quality", type=int, default=95)
+    ap.add_argument("--frames-per-step", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, dist = dist_setup(args.gpus)
+    import torch
+    import guetzli_amd as gz
+
+    dev = local
+    torch.cuda.set_device(dev)
+    w, h, q = args.width, args.height, args.quality
+    params = gz.Params.for_quality(q)
+    nsteps = args.warmup + args.steps
+    # distinct frames per (rank, step, slot), uploaded to HBM before timing
+    frames = []
+    for s in range(nsteps):
+        row = []
+        for f in range(args.frames_per_step):
+            seed = rank * 100000 + s * 100 + f
+            rgb = gz.synthetic_frame(seed, w, h)
+            row.append(torch.from_numpy(rgb.reshape(-1)).to(f"cuda:{dev}"))
+        frames.append(row)
+    torch.cuda.synchronize()
+
+    def step(s):
+        sizes = []
+        out = []
+        for t in frames[s]:
+            data, st = gz.process_device(t.data_ptr(), w, h, params, device=dev, return_stats=True)
+            sizes.append(len(data))
+            out.append(data)
+        if dist is not None:
+            # gather the JPEG byte strings to rank 0 over RCCL/xGMI
+            blob = b"".join(out)
+            n = torch.tensor([len(blob)], dtype=torch.int64, device=f"cuda:{dev}")
+            ns = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(ns, n)
+            mx = int(max(x.item() for x in ns))
+            buf = torch.zeros(mx, dtype=torch.uint8, device=f"cuda:{dev}")
+            buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(buf.device)
+            bufs = [torch.zeros_like(buf) for _ in range(world)]
+            dist.all_gather(bufs, buf)
+        return sizes, st
+
+    for s in range(args.warmup):
+        step(s)
+    gz.profile_reset()
+    gz.profile_enable(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = []
+    host = {}
+    for s in range(args.warmup, nsteps):
+        sizes, st = step(s)
+        iters.append(st.iterations)
+        for k in ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
+                  "seconds_backend", "seconds_compare", "seconds_zeroing"):
+            host[k] = host.get(k, 0.0) + getattr(st, k) / args.steps
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gz.profile_enable(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = gz.profile_read()
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    total_px = world * args.steps * args.frames_per_step * w * h
+    value = total_px / elapsed / 1e6
+
+    # roofline of the dominant HBM-bound kernel of the Butteraugli pass
+    bpp = stage_bytes_per_px()
+    rows = []
+    for name, (cnt, ms) in prof.items():
+        if name in bpp and cnt:
+            rows.append((ms, name, cnt))
+    rows.sort(reverse=True)
+    roof = None
+    stages = {}
+    for ms, name, cnt in rows:
+        avg = ms / cnt
+        gbs = bpp[name] * w * h / (avg * 1e-3) / 1e9
+        stages[name] = {"launches": cnt, "avg_ms": round(avg, 4), "algo_GBps": round(gbs, 1)}
+    if rows:
+        ms, name, cnt = rows[0]
+        avg = ms / cnt
+        achieved = bpp[name] * w * h / (avg * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None, "algo_bytes_per_launch": int(bpp[name] * w * h),
+                "avg_launch_ms": round(avg, 4)}
+    cp = prof.get("compare_pass")
+    pass_bytes = sum(bpp.values()) * w * h
+    compare_pass = None
+    if cp and cp[0]:
+        avg = cp[1] / cp[0]
+        compare_pass = {"launches": cp[0], "avg_ms": round(avg, 4),
+                        "algo_bytes": int(pass_bytes),
+                        "algo_GBps": round(pass_bytes / (avg * 1e-3) / 1e9, 1)}
+    bz = prof.get("block_zeroing")
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "synthetic %dx%d sRGB frame, q=%d, guetzli::Process end to end "
+                               "(BASELINE configs[1])" % (w, h, q),
+                   "width": w, "height": h, "quality": q,
+                   "frames_per_gpu_per_step": args.frames_per_step,
+                   "parallelism": "image-sharded over %d GPU(s)%s" % (
+                       world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
+                   "search_iterations": iters},
+        "roofline": roof,
+        "compare_pass": compare_pass,
+        "block_zeroing": {"launches": bz[0], "avg_ms": round(bz[1] / bz[0], 3)} if bz else None,
+        "stages": stages,
+        "per_frame_seconds": {k: round(v, 4) for k, v in host.items()},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(w, h, q)
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

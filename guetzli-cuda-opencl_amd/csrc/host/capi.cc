@@ -1,6 +1,7 @@
 // extern "C" boundary of libguetzli_hip (include/guetzli_hip.h).
 #include "guetzli_hip.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -156,6 +157,25 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
   return GZ_OK;
 }
 
+void gz_profile_enable(int enable) { gz::ProfileEnable(enable != 0); }
+
+void gz_profile_reset(void) { gz::ProfileReset(); }
+
+int gz_profile_get(const char* name, long* count, double* total_ms) {
+  if (!name || !count || !total_ms) return 0;
+  return gz::ProfileGet(name, count, total_ms) ? 1 : 0;
+}
+
+size_t gz_profile_names(char* buf, size_t cap) {
+  const std::string names = gz::ProfileNames();
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, names.size());
+    std::memcpy(buf, names.data(), n);
+    buf[n] = 0;
+  }
+  return names.size() + 1;
+}
+
 gz_status gz_synthetic_frame(uint64_t seed, int width, int height, uint8_t* rgb_out) {
   if (!rgb_out || width <= 0 || height <= 0)
     return SetError(GZ_ERR_INVALID_ARG, "synthetic_frame: bad argument");
@@ -200,6 +220,10 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
     stats->seconds_compare = res.seconds_compare;
     stats->seconds_zeroing = res.seconds_zeroing;
     stats->seconds_total = res.seconds_total;
+    stats->seconds_setup = res.seconds_setup;
+    stats->seconds_write = res.seconds_write;
+    stats->seconds_quantize = res.seconds_quantize;
+    stats->seconds_backend = res.seconds_backend;
   }
   return GZ_OK;
 }

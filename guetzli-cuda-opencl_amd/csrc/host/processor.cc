@@ -67,7 +67,7 @@ inline int Log2FloorNonZero(uint32_t n) { return 31 ^ __builtin_clz(n); }
 std::unique_ptr<HipButteraugliComparator> HipButteraugliComparator::Create(
     int device, int w, int h, const uint8_t* rgb, bool device_ptr, float target, std::string* err) {
   std::unique_ptr<HipButteraugliComparator> c(new HipButteraugliComparator);
-  c->engine_ = Engine::Create(device, w, h, err);
+  c->engine_ = AcquireEngine(device, w, h, err);
   if (!c->engine_) return nullptr;
   if (!c->engine_->SetReference(rgb, device_ptr)) {
     if (err) *err = c->engine_->error();
@@ -367,8 +367,10 @@ class Processor {
     return false;
   }
   void OutputJpeg(const JpegData& jpg, std::string* out) {
+    const auto t0 = Clock::now();
     out->clear();
     WriteJpeg(jpg, params_.clear_metadata, out);
+    res_->seconds_write += Since(t0);
   }
   void MaybeOutput(const std::string& encoded) {
     const double score = cmp_->ScoreOutputSize(static_cast<int>(encoded.size()));
@@ -399,11 +401,15 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
                                std::string* err) {
   // processor.cc:310-338
   std::memcpy(data->q, q, sizeof(data->q));
+  const auto tq = Clock::now();
   if (!cmp_->QuantizeFromOriginal(q, img)) return Fail(err);
+  res_->seconds_quantize += Since(tq);
   std::string encoded;
   {
+    const auto tw = Clock::now();
     JpegData out = jpg_in;
     img->SaveToJpegData(&out);
+    res_->seconds_write += Since(tw);
     OutputJpeg(out, &encoded);
   }
   ++res_->iterations;
@@ -497,6 +503,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early && direction == -1 && prev_size > 1.01 * res_->jpeg.size()) break;
+      const auto tb = Clock::now();
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
       std::vector<float> block_weight;
@@ -526,7 +533,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
         if (!global_order.empty()) break;
       }
-      if (global_order.empty()) break;
+      if (global_order.empty()) {
+        res_->seconds_backend += Since(tb);
+        break;
+      }
       std::sort(global_order.begin(), global_order.end(),
                 [](const std::pair<int, float>& a, const std::pair<int, float>& b) {
                   return a.second < b.second;
@@ -574,10 +584,13 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
+      res_->seconds_backend += Since(tb);
       std::string encoded;
       {
+        const auto tw = Clock::now();
         JpegData out = jpg;
         img->SaveToJpegData(&out);
+        res_->seconds_write += Since(tw);
         OutputJpeg(out, &encoded);
       }
       if (!cmp_->Compare(*img)) return Fail(err);
@@ -689,6 +702,7 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
       return GZ_ERR_DEVICE;
     }
   }
+  result->seconds_setup = Since(t0);
   const int rc = ProcessJpegData(params, jpg, cmp.get(), result, err);
   if (cmp) {
     result->compares = cmp->compares;

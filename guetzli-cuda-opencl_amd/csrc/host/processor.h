@@ -67,6 +67,7 @@ class HipButteraugliComparator : public Comparator {
   static std::unique_ptr<HipButteraugliComparator> Create(int device, int w, int h,
                                                           const uint8_t* rgb, bool device_ptr,
                                                           float target, std::string* err);
+  ~HipButteraugliComparator() override { ReleaseEngine(std::move(engine_)); }
   bool Compare(const CoeffImage& img) override;
   bool StartBlockComparisons() override;
   void FinishBlockComparisons() override {}
@@ -110,6 +111,11 @@ struct ProcessResult {
   std::string jpeg;
   int iterations = 0, iterations_up = 0, iterations_down = 0, compares = 0;
   double seconds_compare = 0.0, seconds_zeroing = 0.0, seconds_total = 0.0;
+  // host-side breakdown
+  double seconds_setup = 0.0;      // RGB -> q=1 coefficients, engine creation, reference upload
+  double seconds_write = 0.0;      // SaveToJpegData + WriteJpeg per iteration
+  double seconds_quantize = 0.0;   // device quantization + coefficient download
+  double seconds_backend = 0.0;    // SelectFrequencyBackEnd selection / size estimation
 };
 
 // guetzli::Process(params, stats, rgb, w, h, &out) (processor.cc:1157-1185).

@@ -9,7 +9,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+#include <map>
 #include <mutex>
+#include <tuple>
+#include <string>
 #include <vector>
 
 #include "../runtime/engine.h"
@@ -161,6 +165,88 @@ inline dim3 PixGrid(int w, int h, int planes = 1) {
     if (e_ != hipSuccess) return Fail("kernel launch", (int)e_);  \
   } while (0)
 
+// ---------------------------------------------------------------------------
+// Optional per-launch timing with HIP events on the engine's stream
+// (gz_profile_* in the C ABI).  Off by default; when on, every launch is
+// bracketed by two events and the elapsed times are folded into a
+// process-wide table after the call's final stream synchronisation.
+// ---------------------------------------------------------------------------
+namespace {
+std::atomic<int> g_prof_on{0};
+std::mutex g_prof_mu;
+std::map<std::string, std::pair<long, double>> g_prof;
+}  // namespace
+
+void ProfileEnable(bool on) { g_prof_on.store(on ? 1 : 0); }
+void ProfileReset() {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.clear();
+}
+bool ProfileGet(const char* name, long* count, double* total_ms) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  auto it = g_prof.find(name);
+  if (it == g_prof.end()) return false;
+  *count = it->second.first;
+  *total_ms = it->second.second;
+  return true;
+}
+std::string ProfileNames() {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  std::string out;
+  for (auto& kv : g_prof) {
+    if (!out.empty()) out += ",";
+    out += kv.first;
+  }
+  return out;
+}
+
+void Engine::ProfBegin(const char* name) {
+  if (!g_prof_on.load()) return;
+  hipEvent_t a = nullptr, b = nullptr;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+  hipEventRecord(a, static_cast<hipStream_t>(stream_));
+  pending_.push_back({name, a, b});
+}
+void Engine::ProfEnd() {
+  if (pending_.empty() || !g_prof_on.load()) return;
+  hipEventRecord(static_cast<hipEvent_t>(pending_.back().stop), static_cast<hipStream_t>(stream_));
+}
+// Closes the open region `name` (begun with ProfBegin, possibly with other
+// regions recorded in between).
+void Engine::ProfMark(const char* name) {
+  if (!g_prof_on.load()) return;
+  for (auto it = pending_.rbegin(); it != pending_.rend(); ++it)
+    if (it->name == name) {
+      hipEventRecord(static_cast<hipEvent_t>(it->stop), static_cast<hipStream_t>(stream_));
+      return;
+    }
+}
+
+void Engine::ProfFlush() {
+  if (pending_.empty()) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& p : pending_) {
+    float ms = 0.0f;
+    if (hipEventSynchronize(static_cast<hipEvent_t>(p.stop)) == hipSuccess &&
+        hipEventElapsedTime(&ms, static_cast<hipEvent_t>(p.start), static_cast<hipEvent_t>(p.stop)) == hipSuccess) {
+      auto& e = g_prof[p.name];
+      e.first += 1;
+      e.second += ms;
+    }
+    hipEventDestroy(static_cast<hipEvent_t>(p.start));
+    hipEventDestroy(static_cast<hipEvent_t>(p.stop));
+  }
+  pending_.clear();
+}
+
+#define GZ_TIMED(name, ...) \
+  do {                      \
+    ProfBegin(name);        \
+    __VA_ARGS__;            \
+    ProfEnd();              \
+    GZ_LAUNCH();            \
+  } while (0)
+
 bool Engine::Fail(const char* what, int code) {
   char buf[256];
   snprintf(buf, sizeof(buf), "%s failed: %s (%d)", what,
@@ -225,22 +311,50 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_resval_), rn * 4);
   alloc(reinterpret_cast<void**>(&e->d_dd_), n * 4);
   alloc(reinterpret_cast<void**>(&e->d_block_max_), e->nb_ * 4);
-  alloc(reinterpret_cast<void**>(&e->d_gmax_), 16);
   alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
   alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_gmax_), 16) != hipSuccess) ok = false;
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
+    ok = false;
   if (!ok) return fail("device allocation failed");
   return e;
+}
+
+namespace {
+std::mutex g_pool_mu;
+// Intentionally leaked: idle engines must not be freed from a static
+// destructor after the HIP runtime has shut down.
+auto* g_pool = new std::map<std::tuple<int, int, int>, std::vector<std::unique_ptr<Engine>>>;
+constexpr size_t kMaxIdlePerKey = 8;
+}  // namespace
+
+std::unique_ptr<Engine> AcquireEngine(int device, int w, int h, std::string* err) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool->find(std::make_tuple(device, w, h));
+    if (it != g_pool->end() && !it->second.empty()) {
+      std::unique_ptr<Engine> e = std::move(it->second.back());
+      it->second.pop_back();
+      return e;
+    }
+  }
+  return Engine::Create(device, w, h, err);
+}
+
+void ReleaseEngine(std::unique_ptr<Engine> e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto& v = (*g_pool)[std::make_tuple(e->device(), e->width(), e->height())];
+  if (v.size() < kMaxIdlePerKey) v.push_back(std::move(e));
 }
 
 Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
-                  d_dd_, d_block_max_, d_gmax_, d_mask_scale_, d_zero_out_};
+                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (h_gmax_) hipHostFree(h_gmax_);
+  if (h_block_max_) hipHostFree(h_block_max_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
 
@@ -248,19 +362,17 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   GZ_HIP(hipMemcpyAsync(d_rgb_, rgb, 3 * n_, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
-  k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_rgb_, n_, d_lin_);
-  GZ_LAUNCH();
+  GZ_TIMED("ref_linear", k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_rgb_, n_, d_lin_));
   BlurPlanes bp{};
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_lin_ + c * n_;
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigOpsin;
   }
-  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
-  k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_);
-  GZ_LAUNCH();
+  GZ_TIMED("ref_opsin_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_));
   GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   have_mask_scale_ = false;
   return true;
 }
@@ -271,6 +383,7 @@ bool Engine::SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr) {
   GZ_HIP(hipMemcpyAsync(d_orig_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
                         device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   return true;
 }
 
@@ -288,39 +401,33 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   QuantMatrix qm;
   memcpy(qm.q, q, sizeof(qm.q));
   const size_t per = static_cast<size_t>(nb_) * 64;
-  k_quantize<<<dim3((per + 255) / 256, 3), 256, 0, s>>>(d_orig_, qm, per, d_cur_);
-  GZ_LAUNCH();
+  GZ_TIMED("quantize", k_quantize<<<dim3((per + 255) / 256, 3), 256, 0, s>>>(d_orig_, qm, per, d_cur_));
   if (host_out) {
     GZ_HIP(hipMemcpyAsync(host_out, d_cur_, 3 * per * sizeof(int16_t), hipMemcpyDeviceToHost, s));
     GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   }
   return true;
 }
 
 bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  k_diff_precompute<<<PixGrid(w_, h_), 256, 0, s>>>(xyb0, xyb1, w_, h_, d_ma_);
-  GZ_LAUNCH();
-  k_average5x5<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_);
-  GZ_LAUNCH();
-  k_min4_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_mb_, w_, h_, d_ma_);
-  GZ_LAUNCH();
-  k_min4_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_);
-  GZ_LAUNCH();
+  GZ_TIMED("mask_diff_precompute", k_diff_precompute<<<PixGrid(w_, h_), 256, 0, s>>>(xyb0, xyb1, w_, h_, d_ma_));
+  GZ_TIMED("mask_average5x5", k_average5x5<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_));
+  GZ_TIMED("mask_min4_v", k_min4_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_mb_, w_, h_, d_ma_));
+  GZ_TIMED("mask_min4_h", k_min4_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_));
   BlurPlanes bp{};
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_mb_ + c * n_;
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigMaskX + c;
   }
-  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
+  GZ_TIMED("mask_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  k_blur_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
+  GZ_TIMED("mask_blur_v", k_blur_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
   return true;
 }
 
@@ -333,13 +440,12 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     GZ_HIP(hipMemcpyAsync(dst, src, count * 4, hipMemcpyDeviceToHost, s));
     return true;
   };
+  ProfBegin("compare_pass");
   GZ_HIP(hipMemsetAsync(d_edge_, 0, 3 * rn * 4, s));
   GZ_HIP(hipMemsetAsync(d_dc_, 0, 3 * rn * 4, s));
   GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
-  GZ_HIP(hipMemsetAsync(d_gmax_, 0, 4, s));
   // S0: candidate coefficients -> linear RGB
-  k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_);
-  GZ_LAUNCH();
+  GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_));
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
   // S1/S2: opsin dynamics
   BlurPlanes bp{};
@@ -348,14 +454,11 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.out[c] = d_tmp_ + c * n;
     bp.sig[c] = kSigOpsin;
   }
-  k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
-  k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_);
-  GZ_LAUNCH();
+  GZ_TIMED("opsin_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_));
   if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   // S3: high intensity change masking
-  k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_);
-  GZ_LAUNCH();
+  GZ_TIMED("mhic", k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_));
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
   if (dbg && !d2h(dbg->mhic1, d_m1_, 3 * n)) return false;
   // S4/S5: edge detector map
@@ -368,21 +471,17 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[c] = sig;
     bp.sig[3 + c] = sig;
   }
-  k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
+  GZ_TIMED("edge_blur_h", k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
   for (int p = 0; p < 6; ++p) {
     bp.in[p] = d_tmp_ + p * n;
     bp.out[p] = d_bl_ + p * n;
   }
-  k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
-  k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_);
-  GZ_LAUNCH();
+  GZ_TIMED("edge_blur_v", k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
-  k_block_diff<<<(static_cast<unsigned>(rn) + kBdPoints - 1) / kBdPoints, 256, 0, s>>>(
-      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_);
-  GZ_LAUNCH();
+  GZ_TIMED("block_diff", k_block_diff<<<(static_cast<unsigned>(rn) + kBdPoints - 1) / kBdPoints, 256, 0, s>>>(
+      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_));
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
   // S7/S8: low-frequency edge term (sigma 14, step 4)
@@ -393,8 +492,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[3 + c] = kSigLowFreq;
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
-  GZ_LAUNCH();
+  GZ_TIMED("lowfreq_blur_h", k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -402,53 +500,48 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_);
-    GZ_LAUNCH();
-    k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_);
-    GZ_LAUNCH();
+    GZ_TIMED("lowfreq_blur_v", k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+    GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
   // S9-S13: activity mask
   if (!MaskPipeline(d_m0_, d_m1_)) return false;
   MaskPlanes mk{{d_ma_, d_ma_ + n, d_ma_ + 2 * n}};
   if (dbg && (dbg->mask || dbg->mask_dc)) {
-    k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_);
-    GZ_LAUNCH();
+    GZ_TIMED("mask_full_dbg", k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_));
     if (!d2h(dbg->mask, d_mb_, 3 * n)) return false;
     if (!d2h(dbg->mask_dc, d_tmp_, 3 * n)) return false;
   }
   // S14/S15: combine channels (+ mask LUTs, + sqrt)
   float* dbg_comb = nullptr;
   if (dbg && dbg->combined) dbg_comb = d_bl_;  // scratch, consumed below
-  k_combine<<<PixGrid(rw_, rh_), 256, 0, s>>>(mk, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_,
-                                               d_resval_, dbg_comb);
-  GZ_LAUNCH();
+  GZ_TIMED("combine", k_combine<<<PixGrid(rw_, rh_), 256, 0, s>>>(mk, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_,
+                                               d_resval_, dbg_comb));
   if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
   // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
   {
     const int wc = w_ - 5, hc = h_ - 5;
     const int st = HostTables().blur[kSigDiffmap].step;
     const int dxc = (wc + st - 1) / st;
-    k_diffmap_blur_h<<<PixGrid(dxc, hc), 256, 0, s>>>(d_resval_, rw_, wc, hc, d_tmp_);
-    GZ_LAUNCH();
+    GZ_TIMED("diffmap_blur_h", k_diffmap_blur_h<<<PixGrid(dxc, hc), 256, 0, s>>>(d_resval_, rw_, wc, hc, d_tmp_));
     BlurPlanes bd{};
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
     bd.sig[0] = kSigDiffmap;
-    k_blur_v<<<PixGrid(dxc, hc), 256, 0, s>>>(bd, wc, hc);
-    GZ_LAUNCH();
+    GZ_TIMED("diffmap_blur_v", k_blur_v<<<PixGrid(dxc, hc), 256, 0, s>>>(bd, wc, hc));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
-    k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
-                                                              dm, d_block_max_, d_gmax_);
-    GZ_LAUNCH();
+    GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
+                                                              dm, d_block_max_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
-  GZ_HIP(hipMemcpyAsync(h_gmax_, d_gmax_, 4, hipMemcpyDeviceToHost, s));
-  if (block_max) GZ_HIP(hipMemcpyAsync(block_max, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
+  ProfMark("compare_pass");
+  GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
-  float d;
-  memcpy(&d, h_gmax_, 4);
+  ProfFlush();
+  float d = 0.0f;
+  for (int b = 0; b < nb_; ++b) d = d < h_block_max_[b] ? h_block_max_[b] : d;
+  if (block_max) memcpy(block_max, h_block_max_, nb_ * 4);
   *distance = d;
   return true;
 }
@@ -460,11 +553,11 @@ bool Engine::StartBlockComparisons(float* mask_scale_host) {
   // high-intensity masking (butteraugli_comparator.cc:72-79).
   if (!MaskPipeline(d_ref_xyb_, d_ref_xyb_)) return false;
   MaskPlanes mk{{d_ma_, d_ma_ + n_, d_ma_ + 2 * n_}};
-  k_mask_scale<<<(nb_ + 255) / 256, 256, 0, s>>>(mk, w_, h_, bw_, nb_, d_mask_scale_);
-  GZ_LAUNCH();
+  GZ_TIMED("mask_scale", k_mask_scale<<<(nb_ + 255) / 256, 256, 0, s>>>(mk, w_, h_, bw_, nb_, d_mask_scale_));
   if (mask_scale_host)
     GZ_HIP(hipMemcpyAsync(mask_scale_host, d_mask_scale_, 3 * nb_ * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   have_mask_scale_ = true;
   return true;
 }
@@ -473,13 +566,13 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
-  k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
-                                     static_cast<CoeffData*>(d_zero_out_));
-  GZ_LAUNCH();
+                                     static_cast<CoeffData*>(d_zero_out_)));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   return true;
 }
 

@@ -13,6 +13,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace gz {
 
@@ -43,6 +44,7 @@ class Engine {
   static std::unique_ptr<Engine> Create(int device, int w, int h, std::string* err);
   ~Engine();
 
+  int device() const { return device_; }
   int width() const { return w_; }
   int height() const { return h_; }
   int blocks() const { return nb_; }
@@ -72,6 +74,16 @@ class Engine {
  private:
   Engine() = default;
   bool Fail(const char* what, int code);
+  void ProfBegin(const char* name);
+  void ProfEnd();
+  void ProfMark(const char* name);
+  void ProfFlush();
+  struct PendingEvent {
+    std::string name;
+    void* start;
+    void* stop;
+  };
+  std::vector<PendingEvent> pending_;
   bool MaskPipeline(const float* xyb0, const float* xyb1);
 
   int device_ = 0;
@@ -100,12 +112,23 @@ class Engine {
   float* d_resval_ = nullptr;
   float* d_dd_ = nullptr;
   float* d_block_max_ = nullptr;
-  unsigned* d_gmax_ = nullptr;
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
   // pinned host staging
-  unsigned* h_gmax_ = nullptr;
+  float* h_block_max_ = nullptr;
 };
+
+// Process-wide pool of idle engines keyed by (device, width, height): an
+// encode reuses the HBM buffers, stream and tables of an earlier encode of
+// the same size instead of re-allocating ~40 planes.
+std::unique_ptr<Engine> AcquireEngine(int device, int w, int h, std::string* err);
+void ReleaseEngine(std::unique_ptr<Engine> e);
+
+// Per-launch HIP-event timing (off by default).
+void ProfileEnable(bool on);
+void ProfileReset();
+bool ProfileGet(const char* name, long* count, double* total_ms);
+std::string ProfileNames();
 
 // Version / build string of the device library.
 const char* BuildInfo();

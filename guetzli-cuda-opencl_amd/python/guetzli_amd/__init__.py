@@ -48,7 +48,9 @@ class _Stats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int), ("iterations_up", ctypes.c_int),
                 ("iterations_down", ctypes.c_int), ("compares", ctypes.c_int),
                 ("seconds_compare", ctypes.c_double), ("seconds_zeroing", ctypes.c_double),
-                ("seconds_total", ctypes.c_double)]
+                ("seconds_total", ctypes.c_double), ("seconds_setup", ctypes.c_double),
+                ("seconds_write", ctypes.c_double), ("seconds_quantize", ctypes.c_double),
+                ("seconds_backend", ctypes.c_double)]
 
 
 _STAGE_FIELDS = ("cand_linear", "cand_xyb", "mhic0", "mhic1", "edge", "block_dc", "block_ac",
@@ -69,6 +71,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
+    "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
 )
 
 _lib = None
@@ -117,6 +120,12 @@ def lib():
     L.gz_synthetic_frame.restype = i32
     L.gz_rgb_to_coeffs.argtypes = [vp, i32, i32, vp]
     L.gz_rgb_to_coeffs.restype = i32
+    L.gz_profile_enable.argtypes = [i32]
+    L.gz_profile_get.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long),
+                                 ctypes.POINTER(ctypes.c_double)]
+    L.gz_profile_get.restype = i32
+    L.gz_profile_names.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    L.gz_profile_names.restype = ctypes.c_size_t
     _lib = L
     return L
 
@@ -128,6 +137,29 @@ def _check(status, what):
 
 def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def profile_enable(on=True):
+    """Per-launch HIP-event timing inside the library (gz_profile_enable)."""
+    lib().gz_profile_enable(1 if on else 0)
+
+
+def profile_reset():
+    lib().gz_profile_reset()
+
+
+def profile_read():
+    """{region: (count, total_ms)} of everything recorded since the last reset."""
+    L = lib()
+    n = L.gz_profile_names(None, 0)
+    buf = ctypes.create_string_buffer(n)
+    L.gz_profile_names(buf, n)
+    out = {}
+    for name in filter(None, buf.value.decode().split(",")):
+        c, t = ctypes.c_long(), ctypes.c_double()
+        if L.gz_profile_get(name.encode(), ctypes.byref(c), ctypes.byref(t)):
+            out[name] = (c.value, t.value)
+    return out
 
 
 def device_count():
@@ -174,6 +206,10 @@ class ProcessStats:
     seconds_compare: float
     seconds_zeroing: float
     seconds_total: float
+    seconds_setup: float = 0.0
+    seconds_write: float = 0.0
+    seconds_quantize: float = 0.0
+    seconds_backend: float = 0.0
 
 
 def _as_rgb(rgb, width, height):
@@ -199,7 +235,8 @@ def process(rgb, width, height, params=None, device=0, return_stats=False):
     if return_stats:
         return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
                                   st.compares, st.seconds_compare, st.seconds_zeroing,
-                                  st.seconds_total)
+                                  st.seconds_total, st.seconds_setup, st.seconds_write,
+                                  st.seconds_quantize, st.seconds_backend)
     return data
 
 
@@ -218,7 +255,8 @@ def process_device(rgb_dev_ptr, width, height, params=None, device=0, return_sta
     if return_stats:
         return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
                                   st.compares, st.seconds_compare, st.seconds_zeroing,
-                                  st.seconds_total)
+                                  st.seconds_total, st.seconds_setup, st.seconds_write,
+                                  st.seconds_quantize, st.seconds_backend)
     return data
 
 

@@ -69,6 +69,10 @@ typedef struct {
   double seconds_compare;   /* wall time inside Compare calls */
   double seconds_zeroing;   /* wall time of the per-block search */
   double seconds_total;
+  double seconds_setup;     /* initial coefficients, device context, reference */
+  double seconds_write;     /* JPEG serialisation of every candidate */
+  double seconds_quantize;  /* device quantization + coefficient download */
+  double seconds_backend;   /* host coefficient selection / size estimation */
 } gz_process_stats;
 
 /* Stage dumps of one compare (parity tests); any pointer may be NULL.
@@ -139,6 +143,18 @@ gz_status gz_comparator_start_block_comparisons(gz_comparator* cmp, float* mask_
 gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* cur_coeffs,
                                              const int16_t* orig_coeffs, int comp_mask,
                                              float limit, int lookahead, gz_coeff_data* out);
+
+/* ---- measurement ------------------------------------------------------ */
+/* Per-launch timing with HIP events on each object's own stream (off by
+ * default).  Regions are named after the pass stage ("block_diff",
+ * "mask_blur_h", "block_zeroing", ... and "compare_pass" for a whole
+ * Butteraugli pass). */
+void gz_profile_enable(int enable);
+void gz_profile_reset(void);
+/* Returns 1 and fills count / total milliseconds if `name` was recorded. */
+int gz_profile_get(const char* name, long* count, double* total_ms);
+/* Comma-separated recorded region names; returns the length needed. */
+size_t gz_profile_names(char* buf, size_t cap);
 
 /* ---- helpers used by the host search loop ----------------------------- */
 /* Synthetic sRGB test frame (SURVEY.md §8d generator), 3*w*h bytes. */

@@ -46,7 +46,10 @@ def host_e2e_bin():
     src = os.path.join(ROOT, "tests", "native", "host_oracle_e2e.cc")
     lib_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib")
     oracle_dir = os.path.join(ROOT, "oracle", "_build")
-    if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+    deps = [src, os.path.join(lib_dir, "libguetzli_hip.so"),
+            os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host", "processor.h"),
+            os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host", "jpeg_model.h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
         subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
                         "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
