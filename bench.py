@@ -179,6 +179,8 @@ def main():
         for k in ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
                   "seconds_backend", "seconds_compare", "seconds_zeroing"):
             host[k] = host.get(k, 0.0) + getattr(st, k) / args.steps
+        for k, v in gz.last_process_detail().items():
+            host[k] = host.get(k, 0.0) + v / args.steps
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -19,6 +20,7 @@
 namespace {
 
 thread_local std::string g_last_error;
+thread_local std::string g_last_detail = "{}";
 
 gz_status SetError(gz_status st, const std::string& msg) {
   g_last_error = msg;
@@ -157,6 +159,15 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
   return GZ_OK;
 }
 
+size_t gz_last_process_detail(char* buf, size_t cap) {
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, g_last_detail.size());
+    std::memcpy(buf, g_last_detail.data(), n);
+    buf[n] = 0;
+  }
+  return g_last_detail.size() + 1;
+}
+
 void gz_profile_enable(int enable) { gz::ProfileEnable(enable != 0); }
 
 void gz_profile_reset(void) { gz::ProfileReset(); }
@@ -212,6 +223,15 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
   std::memcpy(buf, res.jpeg.data(), res.jpeg.size());
   *jpeg_out = buf;
   *jpeg_size = res.jpeg.size();
+  {
+    std::string j = "{";
+    char item[96];
+    for (auto& kv : res.detail) {
+      snprintf(item, sizeof(item), "%s\"%s\": %.6g", j.size() > 1 ? ", " : "", kv.first.c_str(), kv.second);
+      j += item;
+    }
+    g_last_detail = j + "}";
+  }
   if (stats) {
     stats->iterations = res.iterations;
     stats->iterations_up = res.iterations_up;

@@ -108,6 +108,26 @@ bool CoeffImage::ComponentIsAllZero(int c) const {
   return true;
 }
 
+void CoeffImage::SaveHeaderToJpegData(int ncomp, JpegData* jpg) const {
+  jpg->width = width;
+  jpg->height = height;
+  jpg->max_h_samp_factor = 1;
+  jpg->max_v_samp_factor = 1;
+  jpg->mcu_cols = block_w;
+  jpg->mcu_rows = block_h;
+  jpg->components.resize(ncomp);
+  for (int c = 0; c < ncomp; ++c) {
+    JpegComponent& comp = jpg->components[c];
+    comp.id = c;
+    comp.h_samp_factor = 1;
+    comp.v_samp_factor = 1;
+    comp.width_in_blocks = block_w;
+    comp.height_in_blocks = block_h;
+    comp.coeffs.clear();
+  }
+  SaveQuantTables(quant, jpg);
+}
+
 void CoeffImage::SaveToJpegData(JpegData* jpg) const {
   jpg->width = width;
   jpg->height = height;

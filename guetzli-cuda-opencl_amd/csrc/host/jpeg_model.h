@@ -73,6 +73,9 @@ struct CoeffImage {
   void ApplyGlobalQuantization(const int q[3][kDCTBlockSize]);
   // SaveToJpegData (output_image.cc:579-640)
   void SaveToJpegData(JpegData* jpg) const;
+  // Everything SaveToJpegData sets except the coefficient arrays (left empty),
+  // for a component count already known.
+  void SaveHeaderToJpegData(int ncomp, JpegData* jpg) const;
   bool ComponentIsAllZero(int c) const;
 };
 

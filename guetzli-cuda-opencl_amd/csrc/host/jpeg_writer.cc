@@ -4,6 +4,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "host/thread_pool.h"
+
 namespace gz {
 
 namespace {
@@ -160,22 +162,23 @@ int JpegHistogram::NumSymbols() const {
 void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t* depth) {
   // Huffman tree with iterative count flattening until it fits max_depth
   // (CreateHuffmanTree, entropy_encode.cc:65-145).  Leaves sorted by
-  // (count asc, symbol desc): a total order, so any correct sort agrees.
-  std::vector<TreeNode> tree(2 * length + 1);
+  // (count asc, symbol desc): a total order, so any correct sort agrees --
+  // here a sort of packed 64-bit keys.
+  TreeNode tree[2 * JpegHistogram::kSize + 2];
+  uint64_t keys[JpegHistogram::kSize];
   for (uint32_t count_limit = 1;; count_limit *= 2) {
     int n = 0;
     for (int i = length - 1; i >= 0; --i) {
-      if (data[i]) {
-        tree[n++] = TreeNode{std::max(data[i], count_limit), -1, static_cast<int16_t>(i)};
-      }
+      if (data[i]) keys[n++] = (static_cast<uint64_t>(std::max(data[i], count_limit)) << 16) | (0xffff - i);
     }
     if (n == 1) {
-      depth[tree[0].right_or_value] = 1;
+      depth[0xffff - (keys[0] & 0xffff)] = 1;
       break;
     }
-    std::sort(tree.begin(), tree.begin() + n, [](const TreeNode& a, const TreeNode& b) {
-      return a.total != b.total ? a.total < b.total : a.right_or_value > b.right_or_value;
-    });
+    std::sort(keys, keys + n);
+    for (int k = 0; k < n; ++k)
+      tree[k] = TreeNode{static_cast<uint32_t>(keys[k] >> 16), -1,
+                         static_cast<int16_t>(0xffff - (keys[k] & 0xffff))};
     const TreeNode sentinel{~0u, -1, -1};
     tree[n] = sentinel;
     tree[n + 1] = sentinel;
@@ -190,7 +193,7 @@ void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t
       tree[parent].right_or_value = static_cast<int16_t>(right);
       tree[parent + 1] = sentinel;
     }
-    if (AssignDepths(2 * n - 1, tree.data(), depth, max_depth)) break;
+    if (AssignDepths(2 * n - 1, tree, depth, max_depth)) break;
   }
 }
 
@@ -285,10 +288,11 @@ size_t ClusterHistograms(JpegHistogram* histo, size_t* num, int* idx, uint8_t* d
   return (total + 7) / 8;
 }
 
-bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
+namespace {
+
+// SOI, metadata, DQT and SOF1 (jpeg_data_writer.cc:53-128).
+bool WriteHeaderSegments(const JpegData& jpg, bool strip_metadata, std::string* out) {
   const int ncomps = static_cast<int>(jpg.components.size());
-  if (ncomps < 1 || ncomps > 4) return false;
-  // SOI + metadata (EncodeMetadata, jpeg_data_writer.cc:53-75)
   out->append("\xff\xd8", 2);
   if (strip_metadata) {
     static const unsigned char kApp0[] = {0xff, 0xe0, 0x00, 0x10, 0x4a, 0x46, 0x49, 0x46, 0x00,
@@ -304,7 +308,6 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
       out->append(c);
     }
   }
-  // DQT (jpeg_data_writer.cc:77-100)
   {
     size_t len = 2;
     for (const QuantTable& q : jpg.quant) len += 1 + (q.precision ? 2 : 1) * 64;
@@ -319,76 +322,193 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
       }
     }
   }
-  // SOF1 (jpeg_data_writer.cc:102-128)
-  {
-    out->append("\xff\xc1", 2);
-    Put16(out, 8 + 3 * ncomps);
-    out->push_back(8);
-    Put16(out, jpg.height);
-    Put16(out, jpg.width);
-    out->push_back(static_cast<char>(ncomps));
-    for (const JpegComponent& c : jpg.components) {
-      if (c.quant_idx < 0 || static_cast<size_t>(c.quant_idx) >= jpg.quant.size()) return false;
-      out->push_back(static_cast<char>(c.id));
-      out->push_back(static_cast<char>((c.h_samp_factor << 4) | c.v_samp_factor));
-      out->push_back(static_cast<char>(jpg.quant[c.quant_idx].index));
+  out->append("\xff\xc1", 2);
+  Put16(out, 8 + 3 * ncomps);
+  out->push_back(8);
+  Put16(out, jpg.height);
+  Put16(out, jpg.width);
+  out->push_back(static_cast<char>(ncomps));
+  for (const JpegComponent& c : jpg.components) {
+    if (c.quant_idx < 0 || static_cast<size_t>(c.quant_idx) >= jpg.quant.size()) return false;
+    out->push_back(static_cast<char>(c.id));
+    out->push_back(static_cast<char>((c.h_samp_factor << 4) | c.v_samp_factor));
+    out->push_back(static_cast<char>(jpg.quant[c.quant_idx].index));
+  }
+  return true;
+}
+
+// DHT + SOS from the per-component DC/AC histograms (ncomps entries each;
+// clobbered by clustering) -- BuildAndEncodeHuffmanCodes,
+// jpeg_data_writer.cc:361-445.
+void WriteHuffmanSegments(const JpegData& jpg, JpegHistogram* dc_h, JpegHistogram* ac_h,
+                          HuffTable* dc_tab, HuffTable* ac_tab, std::string* out) {
+  const int ncomps = static_cast<int>(jpg.components.size());
+  std::vector<JpegHistogram> histo(dc_h, dc_h + ncomps);
+  size_t num_dc = ncomps;
+  int dc_idx[4], ac_idx[4];
+  std::vector<uint8_t> depths(ncomps * JpegHistogram::kSize);
+  ClusterHistograms(histo.data(), &num_dc, dc_idx, depths.data());
+  histo.resize(num_dc);
+  histo.insert(histo.end(), ac_h, ac_h + ncomps);
+  depths.resize((num_dc + ncomps) * JpegHistogram::kSize);
+  size_t num_ac = ncomps;
+  ClusterHistograms(&histo[num_dc], &num_ac, ac_idx, &depths[num_dc * JpegHistogram::kSize]);
+  const size_t num_histo = num_dc + num_ac;
+  histo.resize(num_histo);
+  size_t total_symbols = 0;
+  for (const JpegHistogram& h : histo) total_symbols += h.NumSymbols();
+  out->append("\xff\xc4", 2);
+  Put16(out, 2 + num_histo * 17 + total_symbols);
+  for (size_t i = 0; i < num_histo; ++i) {
+    const bool is_dc = i < num_dc;
+    const int id = static_cast<int>(is_dc ? i : i - num_dc);
+    int counts[17] = {0};
+    int values[JpegHistogram::kSize] = {0};
+    BuildCodeCounts(&depths[i * JpegHistogram::kSize], counts, values);
+    HuffTable t;
+    std::memset(t.depth, 255, sizeof(t.depth));
+    std::memset(t.code, 0, sizeof(t.code));
+    BuildCodeTable(counts, values, &t);
+    for (int c = 0; c < ncomps; ++c) {
+      if (is_dc && dc_idx[c] == id) dc_tab[c] = t;
+      if (!is_dc && ac_idx[c] == id) ac_tab[c] = t;
+    }
+    int max_len = 16;
+    while (max_len > 0 && counts[max_len] == 0) --max_len;
+    --counts[max_len];
+    int nsym = 0;
+    for (int j = 0; j <= max_len; ++j) nsym += counts[j];
+    out->push_back(static_cast<char>(is_dc ? i : i - num_dc + 0x10));
+    for (int j = 1; j <= 16; ++j) out->push_back(static_cast<char>(counts[j]));
+    for (int j = 0; j < nsym; ++j) out->push_back(static_cast<char>(values[j]));
+  }
+  out->append("\xff\xda", 2);
+  Put16(out, 6 + 2 * ncomps);
+  out->push_back(static_cast<char>(ncomps));
+  for (int c = 0; c < ncomps; ++c) {
+    out->push_back(static_cast<char>(jpg.components[c].id));
+    out->push_back(static_cast<char>((dc_idx[c] << 4) | ac_idx[c]));
+  }
+  out->push_back(0);
+  out->push_back(63);
+  out->push_back(0);
+}
+
+// One block of the sequential scan (EncodeDCTBlockSequential,
+// jpeg_data_writer.cc:447-500).  `at(k)` yields the coefficient at zigzag
+// position k.
+template <class Sink, class At>
+inline void EncodeBlock(Sink& bw, const At& at, coeff_t* last_dc, const HuffTable& dct,
+                        const HuffTable& act) {
+  const coeff_t dc = at(0);
+  coeff_t diff = static_cast<coeff_t>(dc - *last_dc);
+  *last_dc = dc;
+  coeff_t bits = diff;
+  if (diff < 0) {
+    diff = static_cast<coeff_t>(-diff);
+    --bits;
+  }
+  const int nb = Log2Floor(static_cast<uint32_t>(static_cast<int>(diff))) + 1;
+  bw.Put(dct.depth[nb], static_cast<uint64_t>(dct.code[nb]));
+  if (nb > 0) bw.Put(nb, static_cast<uint64_t>(bits & ((1 << nb) - 1)));
+  int r = 0;
+  for (int k = 1; k < 64; ++k) {
+    coeff_t v = at(k);
+    if (v == 0) {
+      ++r;
+      continue;
+    }
+    coeff_t vb;
+    if (v < 0) {
+      v = static_cast<coeff_t>(-v);
+      vb = static_cast<coeff_t>(~v);
+    } else {
+      vb = v;
+    }
+    while (r > 15) {
+      bw.Put(act.depth[0xf0], static_cast<uint64_t>(act.code[0xf0]));
+      r -= 16;
+    }
+    const int nbits = Log2FloorNonZero(static_cast<uint32_t>(static_cast<int>(v))) + 1;
+    const int sym = (r << 4) + nbits;
+    bw.Put(act.depth[sym], static_cast<uint64_t>(act.code[sym]));
+    bw.Put(nbits, static_cast<uint64_t>(vb & ((1 << nbits) - 1)));
+    r = 0;
+  }
+  if (r > 0) bw.Put(act.depth[0], static_cast<uint64_t>(act.code[0]));
+}
+
+// Unstuffed MSB-first bit buffer: chunks of the scan are encoded into these
+// in parallel and concatenated afterwards.
+struct RawBits {
+  std::vector<uint64_t> words;
+  uint64_t acc = 0;
+  int used = 0;
+  void Clear() {
+    words.clear();
+    acc = 0;
+    used = 0;
+  }
+  void Put(int n, uint64_t bits) {  // 0 <= n <= 64, bits < 2^n
+    if (n == 0) return;
+    const int free = 64 - used;
+    if (n < free) {
+      acc |= bits << (free - n);
+      used += n;
+    } else {
+      const int rem = n - free;
+      acc |= bits >> rem;
+      words.push_back(acc);
+      acc = rem ? (bits << (64 - rem)) : 0;
+      used = rem;
     }
   }
-  // DHT + SOS (BuildAndEncodeHuffmanCodes, jpeg_data_writer.cc:361-445)
+  uint64_t bit_count() const { return 64 * static_cast<uint64_t>(words.size()) + used; }
+};
+
+// Appends the concatenation of `parts`, padded with one bits to a byte
+// boundary and 0xff-stuffed (BitWriter::JumpToByteBoundary + EmitByte).
+void EmitStuffed(const std::vector<RawBits>& parts, int nparts, std::string* out) {
+  RawBits all;
+  uint64_t total = 0;
+  for (int i = 0; i < nparts; ++i) total += parts[i].bit_count();
+  all.words.reserve(total / 64 + 2);
+  for (int i = 0; i < nparts; ++i) {
+    const RawBits& p = parts[i];
+    if (all.used == 0) {
+      all.words.insert(all.words.end(), p.words.begin(), p.words.end());
+    } else {
+      for (uint64_t w : p.words) all.Put(64, w);
+    }
+    if (p.used) all.Put(p.used, p.acc >> (64 - p.used));
+  }
+  if (all.used & 7) all.Put(8 - (all.used & 7), (1u << (8 - (all.used & 7))) - 1);
+  const size_t nbytes = all.words.size() * 8 + all.used / 8;
+  out->reserve(out->size() + nbytes + nbytes / 128 + 16);
+  auto emit = [out](uint8_t b) {
+    out->push_back(static_cast<char>(b));
+    if (b == 0xff) out->push_back(0);
+  };
+  for (uint64_t w : all.words)
+    for (int s = 56; s >= 0; s -= 8) emit(static_cast<uint8_t>(w >> s));
+  for (int s = 56; s > 56 - all.used; s -= 8) emit(static_cast<uint8_t>(all.acc >> s));
+}
+
+}  // namespace
+
+bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
+  // WriteJpeg (jpeg_data_writer.cc:540-553)
+  const int ncomps = static_cast<int>(jpg.components.size());
+  if (ncomps < 1 || ncomps > 4) return false;
+  if (!WriteHeaderSegments(jpg, strip_metadata, out)) return false;
   std::vector<HuffTable> dc_tab(ncomps), ac_tab(ncomps);
   {
-    std::vector<JpegHistogram> histo(ncomps);
-    BuildDCHistograms(jpg, histo.data());
-    size_t num_dc = ncomps;
-    int dc_idx[4], ac_idx[4];
-    std::vector<uint8_t> depths(ncomps * JpegHistogram::kSize);
-    ClusterHistograms(histo.data(), &num_dc, dc_idx, depths.data());
-    histo.resize(num_dc + ncomps);
-    depths.resize((num_dc + ncomps) * JpegHistogram::kSize);
-    BuildACHistograms(jpg, &histo[num_dc]);
-    size_t num_ac = ncomps;
-    ClusterHistograms(&histo[num_dc], &num_ac, ac_idx, &depths[num_dc * JpegHistogram::kSize]);
-    const size_t num_histo = num_dc + num_ac;
-    histo.resize(num_histo);
-    size_t total_symbols = 0;
-    for (const JpegHistogram& h : histo) total_symbols += h.NumSymbols();
-    out->append("\xff\xc4", 2);
-    Put16(out, 2 + num_histo * 17 + total_symbols);
-    for (size_t i = 0; i < num_histo; ++i) {
-      const bool is_dc = i < num_dc;
-      const int id = static_cast<int>(is_dc ? i : i - num_dc);
-      int counts[17] = {0};
-      int values[JpegHistogram::kSize] = {0};
-      BuildCodeCounts(&depths[i * JpegHistogram::kSize], counts, values);
-      HuffTable t;
-      std::memset(t.depth, 255, sizeof(t.depth));
-      std::memset(t.code, 0, sizeof(t.code));
-      BuildCodeTable(counts, values, &t);
-      for (int c = 0; c < ncomps; ++c) {
-        if (is_dc && dc_idx[c] == id) dc_tab[c] = t;
-        if (!is_dc && ac_idx[c] == id) ac_tab[c] = t;
-      }
-      int max_len = 16;
-      while (max_len > 0 && counts[max_len] == 0) --max_len;
-      --counts[max_len];
-      int nsym = 0;
-      for (int j = 0; j <= max_len; ++j) nsym += counts[j];
-      out->push_back(static_cast<char>(is_dc ? i : i - num_dc + 0x10));
-      for (int j = 1; j <= 16; ++j) out->push_back(static_cast<char>(counts[j]));
-      for (int j = 0; j < nsym; ++j) out->push_back(static_cast<char>(values[j]));
-    }
-    out->append("\xff\xda", 2);
-    Put16(out, 6 + 2 * ncomps);
-    out->push_back(static_cast<char>(ncomps));
-    for (int c = 0; c < ncomps; ++c) {
-      out->push_back(static_cast<char>(jpg.components[c].id));
-      out->push_back(static_cast<char>((dc_idx[c] << 4) | ac_idx[c]));
-    }
-    out->push_back(0);
-    out->push_back(63);
-    out->push_back(0);
+    std::vector<JpegHistogram> dc_h(ncomps), ac_h(ncomps);
+    BuildDCHistograms(jpg, dc_h.data());
+    BuildACHistograms(jpg, ac_h.data());
+    WriteHuffmanSegments(jpg, dc_h.data(), ac_h.data(), dc_tab.data(), ac_tab.data(), out);
   }
-  // entropy-coded scan (EncodeScan / EncodeDCTBlockSequential, :447-538)
+  // entropy-coded scan (EncodeScan, jpeg_data_writer.cc:502-538)
   {
     BitSink bw(out);
     coeff_t last_dc[4] = {0, 0, 0, 0};
@@ -396,51 +516,141 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
       for (int mx = 0; mx < jpg.mcu_cols; ++mx)
         for (int ci = 0; ci < ncomps; ++ci) {
           const JpegComponent& c = jpg.components[ci];
-          const HuffTable& dct = dc_tab[ci];
-          const HuffTable& act = ac_tab[ci];
           for (int iy = 0; iy < c.v_samp_factor; ++iy)
             for (int ix = 0; ix < c.h_samp_factor; ++ix) {
               const int bidx = (my * c.v_samp_factor + iy) * c.width_in_blocks + mx * c.h_samp_factor + ix;
               const coeff_t* co = &c.coeffs[static_cast<size_t>(bidx) << 6];
-              coeff_t diff = static_cast<coeff_t>(co[0] - last_dc[ci]);
-              last_dc[ci] = co[0];
-              coeff_t bits = diff;
-              if (diff < 0) {
-                diff = static_cast<coeff_t>(-diff);
-                --bits;
-              }
-              const int nb = Log2Floor(static_cast<uint32_t>(static_cast<int>(diff))) + 1;
-              bw.Put(dct.depth[nb], static_cast<uint64_t>(dct.code[nb]));
-              if (nb > 0) bw.Put(nb, static_cast<uint64_t>(bits & ((1 << nb) - 1)));
-              int r = 0;
-              for (int k = 1; k < 64; ++k) {
-                coeff_t v = co[kJPEGNaturalOrder[k]];
-                if (v == 0) {
-                  ++r;
-                  continue;
-                }
-                coeff_t vb;
-                if (v < 0) {
-                  v = static_cast<coeff_t>(-v);
-                  vb = static_cast<coeff_t>(~v);
-                } else {
-                  vb = v;
-                }
-                while (r > 15) {
-                  bw.Put(act.depth[0xf0], static_cast<uint64_t>(act.code[0xf0]));
-                  r -= 16;
-                }
-                const int nbits = Log2FloorNonZero(static_cast<uint32_t>(static_cast<int>(v))) + 1;
-                const int sym = (r << 4) + nbits;
-                bw.Put(act.depth[sym], static_cast<uint64_t>(act.code[sym]));
-                bw.Put(nbits, static_cast<uint64_t>(vb & ((1 << nbits) - 1)));
-                r = 0;
-              }
-              if (r > 0) bw.Put(act.depth[0], static_cast<uint64_t>(act.code[0]));
+              EncodeBlock(bw, [co](int k) { return co[kJPEGNaturalOrder[k]]; }, &last_dc[ci],
+                          dc_tab[ci], ac_tab[ci]);
             }
         }
     bw.Flush();
   }
+  out->append("\xff\xd9", 2);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Direct, multithreaded encode of a CoeffImage (== SaveToJpegData + WriteJpeg)
+// ---------------------------------------------------------------------------
+
+struct ScanScratch {
+  std::vector<coeff_t> zz;  // [3][blocks][64] quantized, zigzag order
+  std::vector<RawBits> parts;
+  std::vector<JpegHistogram> dc, ac;  // [chunk][3]
+  std::vector<uint8_t> nonzero;       // [chunk]: chroma has a non-zero coefficient
+  int chunks = 0, per_chunk = 0;
+};
+
+ScanScratch* NewScanScratch() { return new ScanScratch; }
+void FreeScanScratch(ScanScratch* s) { delete s; }
+
+namespace {
+
+// Quantizes img into s->zz (as SaveToJpegData divides) and accumulates the
+// DC / AC symbol histograms per chunk of blocks, in parallel.
+int QuantizeAndCount(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
+                     JpegHistogram ac[3]) {
+  const int blocks = img.blocks;
+  s->zz.resize(static_cast<size_t>(blocks) * 64 * 3);
+  const int target_chunks = 4 * HostThreads();
+  s->per_chunk = std::max(64, (blocks + target_chunks - 1) / target_chunks);
+  s->chunks = (blocks + s->per_chunk - 1) / s->per_chunk;
+  s->dc.assign(static_cast<size_t>(s->chunks) * 3, JpegHistogram());
+  s->ac.assign(static_cast<size_t>(s->chunks) * 3, JpegHistogram());
+  s->nonzero.assign(s->chunks, 0);
+  ParallelFor(s->chunks, [&](int ch) {
+    const int b0 = ch * s->per_chunk, b1 = std::min(blocks, b0 + s->per_chunk);
+    bool nz = false;
+    for (int c = 0; c < 3; ++c) {
+      const int* q = img.quant[c];
+      // |src| <= 2^15 and q < 2^24: the correctly rounded f32 quotient
+      // truncates to the exact integer quotient (an inexact quotient is at
+      // least 1/q from an integer, the rounding error below 2^-9/q).
+      float qz[64];
+      for (int k = 0; k < 64; ++k) qz[k] = static_cast<float>(q[kJPEGNaturalOrder[k]]);
+      JpegHistogram& hdc = s->dc[ch * 3 + c];
+      JpegHistogram& hac = s->ac[ch * 3 + c];
+      coeff_t last = b0 > 0 ? static_cast<coeff_t>(img.block(c, b0 - 1)[0] / q[0]) : 0;
+      for (int b = b0; b < b1; ++b) {
+        const coeff_t* src = img.block(c, b);
+        coeff_t* dst = &s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
+        int any = 0;
+        for (int k = 0; k < 64; ++k) {
+          dst[k] = static_cast<coeff_t>(static_cast<int>(static_cast<float>(src[kJPEGNaturalOrder[k]]) / qz[k]));
+          any |= src[k];
+        }
+        if (c > 0 && any) nz = true;
+        hdc.Add(Log2Floor(std::abs(dst[0] - last)) + 1);
+        last = dst[0];
+        int r = 0;
+        for (int k = 1; k < 64; ++k) {
+          const coeff_t v = dst[k];
+          if (v == 0) {
+            ++r;
+            continue;
+          }
+          while (r > 15) {
+            hac.Add(0xf0);
+            r -= 16;
+          }
+          hac.Add((r << 4) + Log2FloorNonZero(std::abs(v)) + 1);
+          r = 0;
+        }
+        if (r > 0) hac.Add(0);
+      }
+    }
+    s->nonzero[ch] = nz;
+  });
+  bool chroma = false;
+  for (int ch = 0; ch < s->chunks; ++ch) chroma |= s->nonzero[ch] != 0;
+  const int ncomp = chroma ? 3 : 1;
+  for (int c = 0; c < 3; ++c) {
+    dc[c].Clear();
+    ac[c].Clear();
+    if (c >= ncomp) continue;
+    for (int ch = 0; ch < s->chunks; ++ch) {
+      dc[c].AddHistogram(s->dc[ch * 3 + c]);
+      ac[c].AddHistogram(s->ac[ch * 3 + c]);
+    }
+  }
+  return ncomp;
+}
+
+}  // namespace
+
+int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
+                         JpegHistogram ac[3]) {
+  return QuantizeAndCount(img, s, dc, ac);
+}
+
+bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                         ScanScratch* s, std::string* out) {
+  JpegHistogram dc_h[3], ac_h[3];
+  const int ncomps = QuantizeAndCount(img, s, dc_h, ac_h);
+  JpegData hdr;
+  hdr.app_data = meta.app_data;
+  hdr.com_data = meta.com_data;
+  img.SaveHeaderToJpegData(ncomps, &hdr);
+  if (!WriteHeaderSegments(hdr, strip_metadata, out)) return false;
+  HuffTable dc_tab[3], ac_tab[3];
+  WriteHuffmanSegments(hdr, dc_h, ac_h, dc_tab, ac_tab, out);
+  const int blocks = img.blocks;
+  s->parts.resize(s->chunks);
+  ParallelFor(s->chunks, [&](int ch) {
+    RawBits& bw = s->parts[ch];
+    bw.Clear();
+    const int b0 = ch * s->per_chunk, b1 = std::min(blocks, b0 + s->per_chunk);
+    coeff_t last_dc[3];
+    for (int c = 0; c < ncomps; ++c)
+      last_dc[c] = b0 > 0 ? s->zz[(static_cast<size_t>(c) * blocks + b0 - 1) * 64] : 0;
+    for (int b = b0; b < b1; ++b)
+      for (int c = 0; c < ncomps; ++c) {
+        const coeff_t* zz = &s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
+        EncodeBlock(bw, [zz](int k) { return zz[k]; }, &last_dc[c], dc_tab[c], ac_tab[c]);
+      }
+  });
+  EmitStuffed(s->parts, s->chunks, out);
   out->append("\xff\xd9", 2);
   return true;
 }

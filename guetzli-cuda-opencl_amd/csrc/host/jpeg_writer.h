@@ -39,4 +39,21 @@ size_t ClusterHistograms(JpegHistogram* histo, size_t* num, int* histo_indexes, 
 // WriteJpeg (jpeg_data_writer.cc:540-553).  Appends to *out.
 bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out);
 
+// Reusable scratch of the direct CoeffImage encoder.
+struct ScanScratch;
+ScanScratch* NewScanScratch();
+void FreeScanScratch(ScanScratch* s);
+
+// DC / AC histograms of the quantized coefficients of img as
+// img.SaveToJpegData() would store them (components >= the returned count
+// are cleared); returns that component count (1 when chroma is all zero).
+int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
+                         JpegHistogram ac[3]);
+
+// Byte-identical to { JpegData j = meta; img.SaveToJpegData(&j);
+// WriteJpeg(j, strip_metadata, out); } without materialising j, with the
+// quantization, histogram and scan passes split over the host pool.
+bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                         ScanScratch* s, std::string* out);
+
 }  // namespace gz

@@ -302,26 +302,6 @@ class QuantMatrixGenerator {
   std::vector<QuantData> quants_;
 };
 
-void UpdateACHistogram(int weight, const coeff_t* coeffs, const int* q, JpegHistogram* h) {
-  // processor.cc:491-515
-  int r = 0;
-  for (int k = 1; k < 64; ++k) {
-    const int kn = kJPEGNaturalOrder[k];
-    const coeff_t c = coeffs[kn];
-    if (c == 0) {
-      ++r;
-      continue;
-    }
-    while (r > 15) {
-      h->Add(0xf0, weight);
-      r -= 16;
-    }
-    h->Add((r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1, weight);
-    r = 0;
-  }
-  if (r > 0) h->Add(0, weight);
-}
-
 size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::vector<uint8_t>* depths) {
   // processor.cc:517-536
   std::vector<JpegHistogram> clustered = histograms;
@@ -338,6 +318,52 @@ size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::ve
   return size;
 }
 
+// UpdateACHistogram (processor.cc:491-515) that also keeps raw_bits = sum_i (counts[i]/2) *
+// (depth[i] + (i & 0xf)) -- the pre-rounding term of HistogramEntropyCost --
+// current for fixed depths, so the size estimate is O(1) per change.
+void UpdateACHistogramCost(int weight, const coeff_t* coeffs, const int* q, const uint8_t* depth,
+                           JpegHistogram* h, int64_t* raw_bits) {
+  int r = 0;
+  int64_t delta = 0;
+  for (int k = 1; k < 64; ++k) {
+    const int kn = kJPEGNaturalOrder[k];
+    const coeff_t c = coeffs[kn];
+    if (c == 0) {
+      ++r;
+      continue;
+    }
+    while (r > 15) {
+      h->Add(0xf0, weight);
+      delta += depth[0xf0];
+      r -= 16;
+    }
+    const int sym = (r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1;
+    h->Add(sym, weight);
+    delta += depth[sym] + (sym & 0xf);
+    r = 0;
+  }
+  if (r > 0) {
+    h->Add(0, weight);
+    delta += depth[0];
+  }
+  *raw_bits += weight * delta;
+}
+
+int64_t HistogramRawBits(const JpegHistogram& h, const uint8_t* depth) {
+  int64_t bits = 0;
+  for (int i = 0; i + 1 < JpegHistogram::kSize; ++i)
+    bits += static_cast<int64_t>(h.counts[i] / 2) * (depth[i] + (i & 0xf));
+  return bits;
+}
+
+// EntropyCodedDataSize from the per-histogram raw bit sums
+// (HistogramEntropyCost's rounding applied per histogram).
+int EntropySizeFromRaw(const std::vector<int64_t>& raw) {
+  int64_t bits = 0;
+  for (int64_t b : raw) bits += b + ((b * 3 + 512) >> 10);
+  return static_cast<int>((bits + 7) / 8);
+}
+
 size_t EntropyCodedDataSize(const std::vector<JpegHistogram>& histograms,
                             const std::vector<uint8_t>& depths) {
   size_t bits = 0;
@@ -346,19 +372,10 @@ size_t EntropyCodedDataSize(const std::vector<JpegHistogram>& histograms,
   return (bits + 7) / 8;
 }
 
-size_t EstimateDCSize(const JpegData& jpg) {
-  std::vector<JpegHistogram> h(jpg.components.size());
-  BuildDCHistograms(jpg, h.data());
-  size_t num = h.size();
-  std::vector<int> idx(num);
-  std::vector<uint8_t> depths(num * JpegHistogram::kSize);
-  return ClusterHistograms(h.data(), &num, idx.data(), depths.data());
-}
-
 class Processor {
  public:
   Processor(const ProcessParams& p, Comparator* cmp, ProcessResult* res)
-      : params_(p), cmp_(cmp), res_(res) {}
+      : params_(p), cmp_(cmp), res_(res), scratch_(NewScanScratch(), FreeScanScratch) {}
   int Run(const JpegData& jpg_in, std::string* err);
 
  private:
@@ -370,7 +387,18 @@ class Processor {
     const auto t0 = Clock::now();
     out->clear();
     WriteJpeg(jpg, params_.clear_metadata, out);
-    res_->seconds_write += Since(t0);
+    const double dt = Since(t0);
+    res_->seconds_write += dt;
+    res_->detail["write_jpeg_s"] += dt;
+  }
+  // SaveToJpegData(img) over jpg + OutputJpeg, without the intermediate JpegData.
+  void OutputCoeffImage(const JpegData& jpg, const CoeffImage& img, std::string* out) {
+    const auto t0 = Clock::now();
+    out->clear();
+    WriteCoeffImageJpeg(img, jpg, params_.clear_metadata, scratch_.get(), out);
+    const double dt = Since(t0);
+    res_->seconds_write += dt;
+    res_->detail["write_jpeg_s"] += dt;
   }
   void MaybeOutput(const std::string& encoded) {
     const double score = cmp_->ScoreOutputSize(static_cast<int>(encoded.size()));
@@ -393,6 +421,7 @@ class Processor {
   ProcessParams params_;
   Comparator* cmp_;
   ProcessResult* res_;
+  std::unique_ptr<ScanScratch, void (*)(ScanScratch*)> scratch_;
   double final_score_ = -1;
 };
 
@@ -405,13 +434,7 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
   if (!cmp_->QuantizeFromOriginal(q, img)) return Fail(err);
   res_->seconds_quantize += Since(tq);
   std::string encoded;
-  {
-    const auto tw = Clock::now();
-    JpegData out = jpg_in;
-    img->SaveToJpegData(&out);
-    res_->seconds_write += Since(tw);
-    OutputJpeg(out, &encoded);
-  }
+  OutputCoeffImage(jpg_in, *img, &encoded);
   ++res_->iterations;
   if (!cmp_->Compare(*img)) return Fail(err);
   data->dist_ok = cmp_->DistanceOK(target_mul);
@@ -467,6 +490,7 @@ bool Processor::SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int
   }
   cmp_->FinishBlockComparisons();
   offsets[num_blocks] = static_cast<int>(cand.size());
+  res_->detail["candidates"] = static_cast<double>(cand.size());
   return SelectFrequencyBackEnd(jpg, img, comp_mask, target_mul, stop_early, offsets, cand,
                                 cand_err, err);
 }
@@ -485,16 +509,29 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   std::vector<JpegHistogram> ac_histograms(ncomp);
   int jpg_header_size, dc_size;
   {
-    JpegData out = jpg;
-    img->SaveToJpegData(&out);
+    JpegHistogram dc_h[3], ac_h[3];
+    const int saved = CoeffImageHistograms(*img, scratch_.get(), dc_h, ac_h);
+    JpegData out;
+    out.app_data = jpg.app_data;
+    out.com_data = jpg.com_data;
+    img->SaveHeaderToJpegData(saved, &out);
     jpg_header_size = static_cast<int>(JpegHeaderSize(out, params_.clear_metadata));
-    dc_size = static_cast<int>(EstimateDCSize(out));
-    BuildACHistograms(out, ac_histograms.data());
+    size_t num = saved;
+    int idx[3];
+    std::vector<uint8_t> depths(saved * JpegHistogram::kSize);
+    dc_size = static_cast<int>(ClusterHistograms(dc_h, &num, idx, depths.data()));
+    for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_h[c];
   }
   std::vector<uint8_t> ac_depths;
   int ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
   const int base_size = jpg_header_size + dc_size + ac_histogram_size +
                         static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+  std::vector<int64_t> raw_bits(ncomp);
+  auto refresh_raw = [&]() {
+    for (int c = 0; c < ncomp; ++c)
+      raw_bits[c] = HistogramRawBits(ac_histograms[c], &ac_depths[c * JpegHistogram::kSize]);
+  };
+  refresh_raw();
   int prev_size = base_size;
   std::vector<float> max_block_error(num_blocks, 0.0f);
   std::vector<int> last_indexes(num_blocks, 0);
@@ -533,14 +570,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
         if (!global_order.empty()) break;
       }
+      res_->detail["backend_order_s"] += Since(tb);
+      res_->detail["backend_order_entries"] += static_cast<double>(global_order.size());
       if (global_order.empty()) {
         res_->seconds_backend += Since(tb);
         break;
       }
+      const auto ts = Clock::now();
       std::sort(global_order.begin(), global_order.end(),
                 [](const std::pair<int, float>& a, const std::pair<int, float>& b) {
                   return a.second < b.second;
                 });
+      res_->detail["backend_sort_s"] += Since(ts);
+      const auto tc = Clock::now();
       double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
       if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
       const double min_size_delta = base_size * rel_size_delta;
@@ -556,7 +598,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       float val_threshold = 0.0f;
       int changed_coeffs = 0;
       int est_jpg_size = prev_size;
-      for (size_t i = 0; i < global_order.size(); ++i) {
+      // The size estimate only matters once changed_coeffs > min_coeffs_to_change
+      // and at the last step (it becomes prev_size); the entropy codes it uses
+      // are those of the last i % 10 == 0 step.  Codes of decades that contain
+      // no such step are never read, so they are not built.  Exact.
+      const size_t n_order = global_order.size();
+      for (size_t i = 0; i < n_order; ++i) {
         const int bix = global_order[i].first;
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
@@ -568,31 +615,34 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const int jpg_bix = by * comp.width_in_blocks + bx;
         const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
         coeff_t* block = img->block(c, bix);
-        UpdateACHistogram(-1, block, quant, &ac_histograms[c]);
+        const uint8_t* depth = &ac_depths[c * JpegHistogram::kSize];
+        UpdateACHistogramCost(-1, block, quant, depth, &ac_histograms[c], &raw_bits[c]);
         block[k] = static_cast<coeff_t>(newval);
-        UpdateACHistogram(1, block, quant, &ac_histograms[c]);
+        UpdateACHistogramCost(1, block, quant, depth, &ac_histograms[c], &raw_bits[c]);
         last_indexes[bix] += direction;
         val_threshold = global_order[i].second;
         ++changed_coeffs;
-        if (i % 10 == 0) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
-        est_jpg_size = jpg_header_size + dc_size + ac_histogram_size +
-                       static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+        const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
+        if (i % 10 == 0 &&
+            (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs_to_change)) || i + 10 >= n_order)) {
+          ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+          refresh_raw();
+          ++res_->detail["backend_entropy_codes"];
+        }
+        if (!needed) continue;
+        est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
         if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta)
           break;
       }
+      res_->detail["backend_changes_s"] += Since(tc);
+      res_->detail["backend_changes"] += changed_coeffs;
       ++img->version;
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
       std::string encoded;
-      {
-        const auto tw = Clock::now();
-        JpegData out = jpg;
-        img->SaveToJpegData(&out);
-        res_->seconds_write += Since(tw);
-        OutputJpeg(out, &encoded);
-      }
+      OutputCoeffImage(jpg, *img, &encoded);
       if (!cmp_->Compare(*img)) return Fail(err);
       MaybeOutput(encoded);
       prev_size = est_jpg_size;

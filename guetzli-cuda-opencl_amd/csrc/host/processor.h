@@ -5,6 +5,7 @@
 
 #include <stdint.h>
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -116,6 +117,8 @@ struct ProcessResult {
   double seconds_write = 0.0;      // SaveToJpegData + WriteJpeg per iteration
   double seconds_quantize = 0.0;   // device quantization + coefficient download
   double seconds_backend = 0.0;    // SelectFrequencyBackEnd selection / size estimation
+  // finer breakdown / counters (reported as JSON by gz_last_process_detail)
+  std::map<std::string, double> detail;
 };
 
 // guetzli::Process(params, stats, rgb, w, h, &out) (processor.cc:1157-1185).

@@ -1,0 +1,20 @@
+// Fixed-size host worker pool for the data-parallel host passes of the search
+// loop (scan encoding, histograms, candidate ordering).  One pool per process;
+// ParallelFor calls from different threads are serialised.  The worker count
+// is GZ_HOST_THREADS, else min(16, hardware threads) — 16 being the CPU share
+// a GPU gets on the target nodes.
+#pragma once
+
+#include <stddef.h>
+
+#include <functional>
+
+namespace gz {
+
+int HostThreads();
+
+// Runs fn(i) for i in [0, n) on the pool (the caller takes part) and returns
+// when all are done.  Items are handed out dynamically.
+void ParallelFor(int n, const std::function<void(int)>& fn);
+
+}  // namespace gz

@@ -72,6 +72,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
+    "gz_last_process_detail",
 )
 
 _lib = None
@@ -126,6 +127,8 @@ def lib():
     L.gz_profile_get.restype = i32
     L.gz_profile_names.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     L.gz_profile_names.restype = ctypes.c_size_t
+    L.gz_last_process_detail.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    L.gz_last_process_detail.restype = ctypes.c_size_t
     _lib = L
     return L
 
@@ -160,6 +163,16 @@ def profile_read():
         if L.gz_profile_get(name.encode(), ctypes.byref(c), ctypes.byref(t)):
             out[name] = (c.value, t.value)
     return out
+
+
+def last_process_detail():
+    """Host-side timers / counters of this thread's last process() call."""
+    import json
+    L = lib()
+    n = L.gz_last_process_detail(None, 0)
+    buf = ctypes.create_string_buffer(n)
+    L.gz_last_process_detail(buf, n)
+    return json.loads(buf.value.decode())
 
 
 def device_count():

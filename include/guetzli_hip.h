@@ -155,6 +155,9 @@ void gz_profile_reset(void);
 int gz_profile_get(const char* name, long* count, double* total_ms);
 /* Comma-separated recorded region names; returns the length needed. */
 size_t gz_profile_names(char* buf, size_t cap);
+/* JSON object of host-side timers / counters of this thread's last encode;
+ * returns the length needed. */
+size_t gz_last_process_detail(char* buf, size_t cap);
 
 /* ---- helpers used by the host search loop ----------------------------- */
 /* Synthetic sRGB test frame (SURVEY.md §8d generator), 3*w*h bytes. */

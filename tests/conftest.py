@@ -39,22 +39,35 @@ def gpu_available(gz):
     return gz.device_count() > 0
 
 
+def _native_bin(name, with_oracle):
+    """Builds tests/native/<name>.cc against the product library (and the
+    oracle when with_oracle) if missing or stale."""
+    out = os.path.join(ROOT, "tests", "_build", name)
+    src = os.path.join(ROOT, "tests", "native", name + ".cc")
+    lib_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib")
+    oracle_dir = os.path.join(ROOT, "oracle", "_build")
+    host_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host")
+    deps = [src, os.path.join(lib_dir, "libguetzli_hip.so")] + [
+        os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith(".h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+               "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
+               "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+               src, "-o", out, "-L", lib_dir, "-lguetzli_hip", "-Wl,-rpath," + lib_dir]
+        if with_oracle:
+            cmd += ["-L", oracle_dir, "-lgz_oracle", "-Wl,-rpath," + oracle_dir]
+        subprocess.run(cmd, check=True)
+    return out
+
+
 @pytest.fixture(scope="session")
 def host_e2e_bin():
     """tests/native/host_oracle_e2e: product host loop + CPU-oracle comparator."""
-    out = os.path.join(ROOT, "tests", "_build", "host_oracle_e2e")
-    src = os.path.join(ROOT, "tests", "native", "host_oracle_e2e.cc")
-    lib_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib")
-    oracle_dir = os.path.join(ROOT, "oracle", "_build")
-    deps = [src, os.path.join(lib_dir, "libguetzli_hip.so"),
-            os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host", "processor.h"),
-            os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host", "jpeg_model.h")]
-    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
-        os.makedirs(os.path.dirname(out), exist_ok=True)
-        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
-                        "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
-                        "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
-                        src, "-o", out, "-L", lib_dir, "-lguetzli_hip", "-L", oracle_dir,
-                        "-lgz_oracle", "-Wl,-rpath," + lib_dir, "-Wl,-rpath," + oracle_dir],
-                       check=True)
-    return out
+    return _native_bin("host_oracle_e2e", True)
+
+
+@pytest.fixture(scope="session")
+def writer_check_bin():
+    """tests/native/writer_check: direct parallel encoder vs SaveToJpegData + WriteJpeg."""
+    return _native_bin("writer_check", False)

@@ -125,6 +125,9 @@ int main(int argc, char** argv) {
   FILE* o = fopen(argv[5], "wb");
   fwrite(res.jpeg.data(), 1, res.jpeg.size(), o);
   fclose(o);
-  printf("{\"bytes\": %zu, \"iters\": %d, \"seconds\": %.4f}\n", res.jpeg.size(), res.iterations, dt);
+  printf("{\"bytes\": %zu, \"iters\": %d, \"seconds\": %.4f", res.jpeg.size(), res.iterations, dt);
+  printf(", \"write_s\": %.4f, \"backend_s\": %.4f", res.seconds_write, res.seconds_backend);
+  for (auto& kv : res.detail) printf(", \"%s\": %.6g", kv.first.c_str(), kv.second);
+  printf("}\n");
   return 0;
 }

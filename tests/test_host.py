@@ -7,6 +7,7 @@
 - the product's host search loop, quantizer and JPEG writer, driven by the
   CPU oracle as comparator (tests/native/host_oracle_e2e.cc), reproduce the
   reference's output bytes end to end;
+- the direct multithreaded JPEG writer equals the serial reference-shaped one;
 - the synthetic frame generator is deterministic;
 - without a GPU the compute entry points fail loudly (no CPU fallback).
 """
@@ -77,6 +78,21 @@ def test_host_loop_with_oracle_comparator_bit_exact(host_e2e_bin, name, tmp_path
     info = json.loads(res.stdout)
     assert info["iters"] == e["iters"]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+
+
+@pytest.mark.parametrize("w,h,seed,scale", [(640, 360, 3, 1), (333, 197, 5, 7), (64, 8, 1, 2),
+                                            (1920, 1080, 0, 3)])
+def test_direct_writer_matches_serial_writer(gz, writer_check_bin, tmp_path, w, h, seed, scale):
+    """The multithreaded CoeffImage encoder is byte-identical to
+    SaveToJpegData + WriteJpeg (reference jpeg_data_writer.cc path)."""
+    rgb = tmp_path / "in.rgb"
+    rgb.write_bytes(gz.synthetic_frame(seed, w, h).tobytes())
+    for threads in ("1", "3"):
+        env = dict(os.environ, GZ_HOST_THREADS=threads)
+        res = subprocess.run([writer_check_bin, str(rgb), str(w), str(h), str(scale)], env=env,
+                             capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stdout + res.stderr
+        assert json.loads(res.stdout)["equal"] == 1
 
 
 def test_synthetic_frames_deterministic(gz):
