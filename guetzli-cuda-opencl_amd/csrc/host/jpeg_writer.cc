@@ -496,50 +496,22 @@ void EmitStuffed(const std::vector<RawBits>& parts, int nparts, std::string* out
 
 }  // namespace
 
-bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
-  // WriteJpeg (jpeg_data_writer.cc:540-553)
-  const int ncomps = static_cast<int>(jpg.components.size());
-  if (ncomps < 1 || ncomps > 4) return false;
-  if (!WriteHeaderSegments(jpg, strip_metadata, out)) return false;
-  std::vector<HuffTable> dc_tab(ncomps), ac_tab(ncomps);
-  {
-    std::vector<JpegHistogram> dc_h(ncomps), ac_h(ncomps);
-    BuildDCHistograms(jpg, dc_h.data());
-    BuildACHistograms(jpg, ac_h.data());
-    WriteHuffmanSegments(jpg, dc_h.data(), ac_h.data(), dc_tab.data(), ac_tab.data(), out);
-  }
-  // entropy-coded scan (EncodeScan, jpeg_data_writer.cc:502-538)
-  {
-    BitSink bw(out);
-    coeff_t last_dc[4] = {0, 0, 0, 0};
-    for (int my = 0; my < jpg.mcu_rows; ++my)
-      for (int mx = 0; mx < jpg.mcu_cols; ++mx)
-        for (int ci = 0; ci < ncomps; ++ci) {
-          const JpegComponent& c = jpg.components[ci];
-          for (int iy = 0; iy < c.v_samp_factor; ++iy)
-            for (int ix = 0; ix < c.h_samp_factor; ++ix) {
-              const int bidx = (my * c.v_samp_factor + iy) * c.width_in_blocks + mx * c.h_samp_factor + ix;
-              const coeff_t* co = &c.coeffs[static_cast<size_t>(bidx) << 6];
-              EncodeBlock(bw, [co](int k) { return co[kJPEGNaturalOrder[k]]; }, &last_dc[ci],
-                          dc_tab[ci], ac_tab[ci]);
-            }
-        }
-    bw.Flush();
-  }
-  out->append("\xff\xd9", 2);
-  return true;
-}
-
 // ---------------------------------------------------------------------------
-// Direct, multithreaded encode of a CoeffImage (== SaveToJpegData + WriteJpeg)
+// Staged, multithreaded encode.  Stage: quantize into zigzag order and count
+// DC / AC symbols per chunk of blocks (parallel).  Encode: cluster + Huffman
+// tables (serial, tiny), scan chunks into raw bit buffers (parallel), then
+// concatenate + pad + 0xff-stuff (serial, ~bytes of output).  Only for the
+// one-block-per-MCU (4:4:4) layout; anything else takes the serial writer.
 // ---------------------------------------------------------------------------
 
 struct ScanScratch {
-  std::vector<coeff_t> zz;  // [3][blocks][64] quantized, zigzag order
+  int blocks = 0, ncomp = 0, chunks = 0, per_chunk = 0;
+  std::vector<coeff_t> zz;  // [4][blocks][64] quantized, zigzag order
   std::vector<RawBits> parts;
-  std::vector<JpegHistogram> dc, ac;  // [chunk][3]
-  std::vector<uint8_t> nonzero;       // [chunk]: chroma has a non-zero coefficient
-  int chunks = 0, per_chunk = 0;
+  std::vector<JpegHistogram> dc, ac;  // [chunk][4]
+  std::vector<uint8_t> nonzero;       // [chunk]: some chroma coefficient non-zero
+  JpegData hdr;                       // the staged image without coefficients
+  JpegHistogram dc_h[4], ac_h[4];
 };
 
 ScanScratch* NewScanScratch() { return new ScanScratch; }
@@ -547,40 +519,33 @@ void FreeScanScratch(ScanScratch* s) { delete s; }
 
 namespace {
 
-// Quantizes img into s->zz (as SaveToJpegData divides) and accumulates the
-// DC / AC symbol histograms per chunk of blocks, in parallel.
-int QuantizeAndCount(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
-                     JpegHistogram ac[3]) {
-  const int blocks = img.blocks;
-  s->zz.resize(static_cast<size_t>(blocks) * 64 * 3);
+// load(c, b, zz) writes block b of component c in zigzag order and returns
+// non-zero iff the stored (pre-division) block has a non-zero coefficient.
+template <class Load>
+void StageBlocks(int blocks, int ncomp, ScanScratch* s, const Load& load) {
+  s->blocks = blocks;
+  s->zz.resize(static_cast<size_t>(blocks) * 64 * ncomp);
   const int target_chunks = 4 * HostThreads();
   s->per_chunk = std::max(64, (blocks + target_chunks - 1) / target_chunks);
   s->chunks = (blocks + s->per_chunk - 1) / s->per_chunk;
-  s->dc.assign(static_cast<size_t>(s->chunks) * 3, JpegHistogram());
-  s->ac.assign(static_cast<size_t>(s->chunks) * 3, JpegHistogram());
+  s->dc.assign(static_cast<size_t>(s->chunks) * 4, JpegHistogram());
+  s->ac.assign(static_cast<size_t>(s->chunks) * 4, JpegHistogram());
   s->nonzero.assign(s->chunks, 0);
   ParallelFor(s->chunks, [&](int ch) {
     const int b0 = ch * s->per_chunk, b1 = std::min(blocks, b0 + s->per_chunk);
     bool nz = false;
-    for (int c = 0; c < 3; ++c) {
-      const int* q = img.quant[c];
-      // |src| <= 2^15 and q < 2^24: the correctly rounded f32 quotient
-      // truncates to the exact integer quotient (an inexact quotient is at
-      // least 1/q from an integer, the rounding error below 2^-9/q).
-      float qz[64];
-      for (int k = 0; k < 64; ++k) qz[k] = static_cast<float>(q[kJPEGNaturalOrder[k]]);
-      JpegHistogram& hdc = s->dc[ch * 3 + c];
-      JpegHistogram& hac = s->ac[ch * 3 + c];
-      coeff_t last = b0 > 0 ? static_cast<coeff_t>(img.block(c, b0 - 1)[0] / q[0]) : 0;
+    coeff_t prev[64];
+    for (int c = 0; c < ncomp; ++c) {
+      JpegHistogram& hdc = s->dc[ch * 4 + c];
+      JpegHistogram& hac = s->ac[ch * 4 + c];
+      coeff_t last = 0;
+      if (b0 > 0) {
+        load(c, b0 - 1, prev);
+        last = prev[0];
+      }
       for (int b = b0; b < b1; ++b) {
-        const coeff_t* src = img.block(c, b);
         coeff_t* dst = &s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
-        int any = 0;
-        for (int k = 0; k < 64; ++k) {
-          dst[k] = static_cast<coeff_t>(static_cast<int>(static_cast<float>(src[kJPEGNaturalOrder[k]]) / qz[k]));
-          any |= src[k];
-        }
-        if (c > 0 && any) nz = true;
+        if (load(c, b, dst) && c > 0) nz = true;
         hdc.Add(Log2Floor(std::abs(dst[0] - last)) + 1);
         last = dst[0];
         int r = 0;
@@ -602,46 +567,111 @@ int QuantizeAndCount(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
     }
     s->nonzero[ch] = nz;
   });
-  bool chroma = false;
-  for (int ch = 0; ch < s->chunks; ++ch) chroma |= s->nonzero[ch] != 0;
-  const int ncomp = chroma ? 3 : 1;
-  for (int c = 0; c < 3; ++c) {
-    dc[c].Clear();
-    ac[c].Clear();
-    if (c >= ncomp) continue;
+}
+
+void SumHistograms(ScanScratch* s) {
+  for (int c = 0; c < 4; ++c) {
+    s->dc_h[c].Clear();
+    s->ac_h[c].Clear();
+    if (c >= s->ncomp) continue;
     for (int ch = 0; ch < s->chunks; ++ch) {
-      dc[c].AddHistogram(s->dc[ch * 3 + c]);
-      ac[c].AddHistogram(s->ac[ch * 3 + c]);
+      s->dc_h[c].AddHistogram(s->dc[ch * 4 + c]);
+      s->ac_h[c].AddHistogram(s->ac[ch * 4 + c]);
     }
   }
-  return ncomp;
+}
+
+bool IsOneBlockPerMcu(const JpegData& jpg) {
+  const int n = static_cast<int>(jpg.components.size());
+  if (n < 1 || n > 4) return false;
+  const size_t blocks = static_cast<size_t>(jpg.mcu_cols) * jpg.mcu_rows;
+  for (const JpegComponent& c : jpg.components)
+    if (c.h_samp_factor != 1 || c.v_samp_factor != 1 || c.width_in_blocks != jpg.mcu_cols ||
+        c.coeffs.size() < blocks * 64)
+      return false;
+  return true;
+}
+
+bool WriteJpegSerial(const JpegData& jpg, bool strip_metadata, std::string* out) {
+  const int ncomps = static_cast<int>(jpg.components.size());
+  if (ncomps < 1 || ncomps > 4) return false;
+  if (!WriteHeaderSegments(jpg, strip_metadata, out)) return false;
+  std::vector<HuffTable> dc_tab(ncomps), ac_tab(ncomps);
+  {
+    std::vector<JpegHistogram> dc_h(ncomps), ac_h(ncomps);
+    BuildDCHistograms(jpg, dc_h.data());
+    BuildACHistograms(jpg, ac_h.data());
+    WriteHuffmanSegments(jpg, dc_h.data(), ac_h.data(), dc_tab.data(), ac_tab.data(), out);
+  }
+  // entropy-coded scan (EncodeScan, jpeg_data_writer.cc:502-538)
+  BitSink bw(out);
+  coeff_t last_dc[4] = {0, 0, 0, 0};
+  for (int my = 0; my < jpg.mcu_rows; ++my)
+    for (int mx = 0; mx < jpg.mcu_cols; ++mx)
+      for (int ci = 0; ci < ncomps; ++ci) {
+        const JpegComponent& c = jpg.components[ci];
+        for (int iy = 0; iy < c.v_samp_factor; ++iy)
+          for (int ix = 0; ix < c.h_samp_factor; ++ix) {
+            const int bidx = (my * c.v_samp_factor + iy) * c.width_in_blocks + mx * c.h_samp_factor + ix;
+            const coeff_t* co = &c.coeffs[static_cast<size_t>(bidx) << 6];
+            EncodeBlock(bw, [co](int k) { return co[kJPEGNaturalOrder[k]]; }, &last_dc[ci],
+                        dc_tab[ci], ac_tab[ci]);
+          }
+      }
+  bw.Flush();
+  out->append("\xff\xd9", 2);
+  return true;
 }
 
 }  // namespace
 
-int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
-                         JpegHistogram ac[3]) {
-  return QuantizeAndCount(img, s, dc, ac);
+int StageCoeffImage(const CoeffImage& img, const JpegData& meta, ScanScratch* s) {
+  // Quantization as SaveToJpegData divides (output_image.cc:618-626).
+  // |stored| <= 2^15 and q < 2^24: the correctly rounded f32 quotient
+  // truncates to the exact integer quotient (an inexact quotient is at least
+  // 1/q from an integer, the rounding error below 2^-9/q; checked
+  // exhaustively for q < 2^16).
+  float qz[3][64];
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) qz[c][k] = static_cast<float>(img.quant[c][kJPEGNaturalOrder[k]]);
+  StageBlocks(img.blocks, 3, s, [&](int c, int b, coeff_t* dst) {
+    const coeff_t* src = img.block(c, b);
+    int any = 0;
+    for (int k = 0; k < 64; ++k) {
+      dst[k] = static_cast<coeff_t>(
+          static_cast<int>(static_cast<float>(src[kJPEGNaturalOrder[k]]) / qz[c][k]));
+      any |= src[k];
+    }
+    return any != 0;
+  });
+  bool chroma = false;
+  for (int ch = 0; ch < s->chunks; ++ch) chroma |= s->nonzero[ch] != 0;
+  s->ncomp = chroma ? 3 : 1;  // SaveToJpegData drops all-zero chroma
+  SumHistograms(s);
+  s->hdr.app_data = meta.app_data;
+  s->hdr.com_data = meta.com_data;
+  img.SaveHeaderToJpegData(s->ncomp, &s->hdr);
+  return s->ncomp;
 }
 
-bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
-                         ScanScratch* s, std::string* out) {
-  JpegHistogram dc_h[3], ac_h[3];
-  const int ncomps = QuantizeAndCount(img, s, dc_h, ac_h);
-  JpegData hdr;
-  hdr.app_data = meta.app_data;
-  hdr.com_data = meta.com_data;
-  img.SaveHeaderToJpegData(ncomps, &hdr);
+bool EncodeStaged(ScanScratch* s, bool strip_metadata, std::string* out) {
+  const JpegData& hdr = s->hdr;
+  const int ncomps = s->ncomp;
   if (!WriteHeaderSegments(hdr, strip_metadata, out)) return false;
-  HuffTable dc_tab[3], ac_tab[3];
+  HuffTable dc_tab[4], ac_tab[4];
+  JpegHistogram dc_h[4], ac_h[4];
+  for (int c = 0; c < ncomps; ++c) {
+    dc_h[c] = s->dc_h[c];
+    ac_h[c] = s->ac_h[c];
+  }
   WriteHuffmanSegments(hdr, dc_h, ac_h, dc_tab, ac_tab, out);
-  const int blocks = img.blocks;
+  const int blocks = s->blocks;
   s->parts.resize(s->chunks);
   ParallelFor(s->chunks, [&](int ch) {
     RawBits& bw = s->parts[ch];
     bw.Clear();
     const int b0 = ch * s->per_chunk, b1 = std::min(blocks, b0 + s->per_chunk);
-    coeff_t last_dc[3];
+    coeff_t last_dc[4];
     for (int c = 0; c < ncomps; ++c)
       last_dc[c] = b0 > 0 ? s->zz[(static_cast<size_t>(c) * blocks + b0 - 1) * 64] : 0;
     for (int b = b0; b < b1; ++b)
@@ -653,6 +683,60 @@ bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip
   EmitStuffed(s->parts, s->chunks, out);
   out->append("\xff\xd9", 2);
   return true;
+}
+
+int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
+                         JpegHistogram ac[3]) {
+  JpegData none;
+  const int n = StageCoeffImage(img, none, s);
+  for (int c = 0; c < 3; ++c) {
+    dc[c] = s->dc_h[c];
+    ac[c] = s->ac_h[c];
+  }
+  return n;
+}
+
+bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                         ScanScratch* s, std::string* out) {
+  StageCoeffImage(img, meta, s);
+  return EncodeStaged(s, strip_metadata, out);
+}
+
+bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
+  // WriteJpeg (jpeg_data_writer.cc:540-553)
+  if (!IsOneBlockPerMcu(jpg)) return WriteJpegSerial(jpg, strip_metadata, out);
+  ScanScratch s;
+  const int ncomp = static_cast<int>(jpg.components.size());
+  StageBlocks(jpg.mcu_cols * jpg.mcu_rows, ncomp, &s, [&](int c, int b, coeff_t* dst) {
+    const coeff_t* src = &jpg.components[c].coeffs[static_cast<size_t>(b) * 64];
+    for (int k = 0; k < 64; ++k) dst[k] = src[kJPEGNaturalOrder[k]];
+    return true;
+  });
+  s.ncomp = ncomp;
+  SumHistograms(&s);
+  s.hdr.width = jpg.width;
+  s.hdr.height = jpg.height;
+  s.hdr.mcu_cols = jpg.mcu_cols;
+  s.hdr.mcu_rows = jpg.mcu_rows;
+  s.hdr.app_data = jpg.app_data;
+  s.hdr.com_data = jpg.com_data;
+  s.hdr.quant = jpg.quant;
+  s.hdr.components.resize(ncomp);
+  for (int c = 0; c < ncomp; ++c) {
+    const JpegComponent& src = jpg.components[c];
+    JpegComponent& dst = s.hdr.components[c];
+    dst.id = src.id;
+    dst.h_samp_factor = src.h_samp_factor;
+    dst.v_samp_factor = src.v_samp_factor;
+    dst.quant_idx = src.quant_idx;
+    dst.width_in_blocks = src.width_in_blocks;
+    dst.height_in_blocks = src.height_in_blocks;
+  }
+  return EncodeStaged(&s, strip_metadata, out);
+}
+
+bool WriteJpegReference(const JpegData& jpg, bool strip_metadata, std::string* out) {
+  return WriteJpegSerial(jpg, strip_metadata, out);
 }
 
 }  // namespace gz

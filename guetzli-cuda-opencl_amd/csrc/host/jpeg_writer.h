@@ -36,23 +36,31 @@ void BuildACHistograms(const JpegData& jpg, JpegHistogram* histo);
 size_t JpegHeaderSize(const JpegData& jpg, bool strip_metadata);
 size_t ClusterHistograms(JpegHistogram* histo, size_t* num, int* histo_indexes, uint8_t* depths);
 
-// WriteJpeg (jpeg_data_writer.cc:540-553).  Appends to *out.
+// WriteJpeg (jpeg_data_writer.cc:540-553).  Appends to *out.  4:4:4 input
+// takes the staged multithreaded encoder, anything else the serial one.
 bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out);
+// The serial writer, always (test comparison baseline).
+bool WriteJpegReference(const JpegData& jpg, bool strip_metadata, std::string* out);
 
-// Reusable scratch of the direct CoeffImage encoder.
+// Reusable scratch of the staged encoder.
 struct ScanScratch;
 ScanScratch* NewScanScratch();
 void FreeScanScratch(ScanScratch* s);
 
-// DC / AC histograms of the quantized coefficients of img as
-// img.SaveToJpegData() would store them (components >= the returned count
-// are cleared); returns that component count (1 when chroma is all zero).
+// Stage 1 of encoding { JpegData j = meta; img.SaveToJpegData(&j); } --
+// quantization and symbol counts, parallel.  After it returns img is no longer
+// referenced (the search may keep editing it while EncodeStaged runs).
+// Returns the component count SaveToJpegData keeps (1 if chroma is all zero).
+int StageCoeffImage(const CoeffImage& img, const JpegData& meta, ScanScratch* s);
+// Stage 2: WriteJpeg of the staged image; appends to *out.
+bool EncodeStaged(ScanScratch* s, bool strip_metadata, std::string* out);
+
+// DC / AC histograms of img as SaveToJpegData would store it (components at
+// or above the returned count are cleared); returns that count.
 int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc[3],
                          JpegHistogram ac[3]);
 
-// Byte-identical to { JpegData j = meta; img.SaveToJpegData(&j);
-// WriteJpeg(j, strip_metadata, out); } without materialising j, with the
-// quantization, histogram and scan passes split over the host pool.
+// StageCoeffImage + EncodeStaged: byte-identical to SaveToJpegData + WriteJpeg.
 bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                          ScanScratch* s, std::string* out);
 

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstring>
 #include <set>
+#include <thread>
 #include <utility>
 
 #include <hip/hip_runtime.h>
@@ -17,6 +18,7 @@
 #include "guetzli_hip.h"
 #include "host/jpeg_encode.h"
 #include "host/jpeg_writer.h"
+#include "host/lazy_sort.h"
 
 namespace gz {
 
@@ -337,7 +339,7 @@ void UpdateACHistogramCost(int weight, const coeff_t* coeffs, const int* q, cons
       delta += depth[0xf0];
       r -= 16;
     }
-    const int sym = (r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1;
+    const int sym = (r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1;  // q[kn] != 0
     h->Add(sym, weight);
     delta += depth[sym] + (sym & 0xf);
     r = 0;
@@ -376,6 +378,9 @@ class Processor {
  public:
   Processor(const ProcessParams& p, Comparator* cmp, ProcessResult* res)
       : params_(p), cmp_(cmp), res_(res), scratch_(NewScanScratch(), FreeScanScratch) {}
+  ~Processor() {
+    if (writer_.joinable()) writer_.join();
+  }
   int Run(const JpegData& jpg_in, std::string* err);
 
  private:
@@ -391,14 +396,40 @@ class Processor {
     res_->seconds_write += dt;
     res_->detail["write_jpeg_s"] += dt;
   }
-  // SaveToJpegData(img) over jpg + OutputJpeg, without the intermediate JpegData.
-  void OutputCoeffImage(const JpegData& jpg, const CoeffImage& img, std::string* out) {
+  // Output of a search candidate: SaveToJpegData(img) over jpg + OutputJpeg
+  // + MaybeOutput, pipelined.  BeginOutput stages img (quantize + count, on
+  // the pool) and encodes it on a helper thread while the caller runs the
+  // Compare and, in the back end, the next iteration's selection.  The
+  // MaybeOutput of a candidate must see the distance of the Compare that
+  // followed it, so it is applied by FlushOutput, which runs before the next
+  // Compare (at the next BeginOutput) or explicitly.
+  void BeginOutput(const JpegData& jpg, const CoeffImage& img) {
+    FlushOutput();
     const auto t0 = Clock::now();
-    out->clear();
-    WriteCoeffImageJpeg(img, jpg, params_.clear_metadata, scratch_.get(), out);
+    StageCoeffImage(img, jpg, scratch_.get());
+    pending_.clear();
+    writer_ = std::thread([this] {
+      const auto t = Clock::now();
+      EncodeStaged(scratch_.get(), params_.clear_metadata, &pending_);
+      encode_s_ = Since(t);
+    });
+    has_pending_ = true;
     const double dt = Since(t0);
     res_->seconds_write += dt;
-    res_->detail["write_jpeg_s"] += dt;
+    res_->detail["write_stage_s"] += dt;
+  }
+  // Joins the pending encode and applies its MaybeOutput; returns its size.
+  size_t FlushOutput() {
+    if (!has_pending_) return 0;
+    const auto t0 = Clock::now();
+    writer_.join();
+    const double dt = Since(t0);
+    res_->seconds_write += dt;
+    res_->detail["write_wait_s"] += dt;
+    res_->detail["write_encode_s"] += encode_s_;
+    has_pending_ = false;
+    MaybeOutput(pending_);
+    return pending_.size();
   }
   void MaybeOutput(const std::string& encoded) {
     const double score = cmp_->ScoreOutputSize(static_cast<int>(encoded.size()));
@@ -422,6 +453,10 @@ class Processor {
   Comparator* cmp_;
   ProcessResult* res_;
   std::unique_ptr<ScanScratch, void (*)(ScanScratch*)> scratch_;
+  std::thread writer_;
+  std::string pending_;
+  bool has_pending_ = false;
+  double encode_s_ = 0.0;
   double final_score_ = -1;
 };
 
@@ -433,13 +468,11 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
   const auto tq = Clock::now();
   if (!cmp_->QuantizeFromOriginal(q, img)) return Fail(err);
   res_->seconds_quantize += Since(tq);
-  std::string encoded;
-  OutputCoeffImage(jpg_in, *img, &encoded);
+  BeginOutput(jpg_in, *img);
   ++res_->iterations;
   if (!cmp_->Compare(*img)) return Fail(err);
   data->dist_ok = cmp_->DistanceOK(target_mul);
-  data->jpg_size = encoded.size();
-  MaybeOutput(encoded);
+  data->jpg_size = FlushOutput();
   return true;
 }
 
@@ -539,6 +572,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   bool first_up_iter = true;
   for (int direction : {1, -1}) {
     for (;;) {
+      if (stop_early) FlushOutput();  // res_->jpeg must be current
       if (stop_early && direction == -1 && prev_size > 1.01 * res_->jpeg.size()) break;
       const auto tb = Clock::now();
       std::vector<std::pair<int, float>> global_order;
@@ -576,12 +610,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         res_->seconds_backend += Since(tb);
         break;
       }
-      const auto ts = Clock::now();
-      std::sort(global_order.begin(), global_order.end(),
-                [](const std::pair<int, float>& a, const std::pair<int, float>& b) {
-                  return a.second < b.second;
-                });
-      res_->detail["backend_sort_s"] += Since(ts);
+      // std::sort(global_order) by key (processor.cc:840-843), materialised
+      // lazily: only the prefix the change loop consumes gets sorted.
+      LazyStdSort sorter(global_order.data(), global_order.size());
       const auto tc = Clock::now();
       double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
       if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
@@ -590,9 +621,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
       if (first_up_iter) {
         const float limit = 0.75f * cmp_->BlockErrorLimit();
-        auto it = std::partition_point(global_order.begin(), global_order.end(),
-                                       [=](const std::pair<int, float>& a) { return a.second < limit; });
-        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, static_cast<int>(it - global_order.begin()));
+        // partition_point(key < limit) of the sorted order == count of keys below limit
+        int below = 0;
+        for (const auto& e : global_order) below += e.second < limit ? 1 : 0;
+        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, below);
         first_up_iter = false;
       }
       float val_threshold = 0.0f;
@@ -604,6 +636,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // no such step are never read, so they are not built.  Exact.
       const size_t n_order = global_order.size();
       for (size_t i = 0; i < n_order; ++i) {
+        if (i >= sorter.sorted()) sorter.EnsureSorted(i);
         const int bix = global_order[i].first;
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
@@ -641,13 +674,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
-      std::string encoded;
-      OutputCoeffImage(jpg, *img, &encoded);
+      BeginOutput(jpg, *img);
       if (!cmp_->Compare(*img)) return Fail(err);
-      MaybeOutput(encoded);
       prev_size = est_jpg_size;
     }
   }
+  FlushOutput();
   return true;
 }
 

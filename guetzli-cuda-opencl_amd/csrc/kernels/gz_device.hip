@@ -152,6 +152,27 @@ inline dim3 PixGrid(int w, int h, int planes = 1) {
   return dim3((w + 255) / 256, h, planes);
 }
 
+// Grids sized to the down-sampled outputs of the planes' blurs (the finest
+// step among them decides).
+int MinStep(int planes, const BlurPlanes& bp) {
+  int st = 1 << 20;
+  for (int p = 0; p < planes; ++p) st = std::min(st, HostTables().blur[bp.sig[p]].step);
+  return st;
+}
+inline dim3 BlurHGrid(int w, int h, int planes, const BlurPlanes& bp) {
+  const int st = MinStep(planes, bp);
+  return dim3(((w + st - 1) / st + kBlurTile - 1) / kBlurTile, h, planes);
+}
+inline dim3 BlurVGrid(int w, int h, int planes, const BlurPlanes& bp) {
+  const int st = MinStep(planes, bp);
+  return dim3(((w + st - 1) / st + 255) / 256, (h + st - 1) / st, planes);
+}
+inline RowsPlain Rows(const BlurPlanes& bp) {
+  RowsPlain r{};
+  for (int p = 0; p < 6; ++p) r.in[p] = bp.in[p];
+  return r;
+}
+
 }  // namespace
 
 #define GZ_HIP(call)                                   \
@@ -270,6 +291,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     std::lock_guard<std::mutex> lk(g_tab_mu);
     if (!g_tab_uploaded[device]) {
       const GzTables& t = HostTables();
+      for (const BlurSpec& b : t.blur)
+        if ((kBlurTile - 1) * b.step + 2 * b.radius + 1 + b.step > kBlurLds || 2 * b.radius + 1 > kMaxTaps)
+          return fail("blur spec exceeds the tiled kernel's LDS span");
       if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(t)) != hipSuccess)
         return fail("table upload failed");
       g_tab_uploaded[device] = true;
@@ -313,9 +337,15 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_block_max_), e->nb_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
   alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
+  e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
+  alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
     ok = false;
   if (!ok) return fail("device allocation failed");
+  k_blur_scales<<<dim3((e->scale_stride_ + 255) / 256, kNumSigmas * 2), 256, 0, s>>>(
+      w, h, e->scale_stride_, e->d_scales_);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail("blur scale precompute failed");
   return e;
 }
 
@@ -351,7 +381,7 @@ Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
-                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_};
+                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h_block_max_) hipHostFree(h_block_max_);
@@ -369,8 +399,10 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("ref_opsin_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
-  GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_));
+  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+      Rows(bp), bp, w_, d_scales_, scale_stride_));
+  GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_,
+                                                                      d_scales_, scale_stride_));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
   have_mask_scale_ = false;
@@ -422,12 +454,13 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigMaskX + c;
   }
-  GZ_TIMED("mask_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("mask_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+      Rows(bp), bp, w_, d_scales_, scale_stride_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  GZ_TIMED("mask_blur_v", k_blur_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("mask_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 3, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -454,8 +487,10 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.out[c] = d_tmp_ + c * n;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("opsin_blur_h", k_blur_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(bp, w_, h_));
-  GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_));
+  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+      Rows(bp), bp, w_, d_scales_, scale_stride_));
+  GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_,
+                                                                  d_scales_, scale_stride_));
   if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   // S3: high intensity change masking
   GZ_TIMED("mhic", k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_));
@@ -471,12 +506,13 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[c] = sig;
     bp.sig[3 + c] = sig;
   }
-  GZ_TIMED("edge_blur_h", k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("edge_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+      Rows(bp), bp, w_, d_scales_, scale_stride_));
   for (int p = 0; p < 6; ++p) {
     bp.in[p] = d_tmp_ + p * n;
     bp.out[p] = d_bl_ + p * n;
   }
-  GZ_TIMED("edge_blur_v", k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("edge_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
@@ -492,7 +528,8 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[3 + c] = kSigLowFreq;
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  GZ_TIMED("lowfreq_blur_h", k_blur_h<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+      Rows(bp), bp, w_, d_scales_, scale_stride_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -500,7 +537,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    GZ_TIMED("lowfreq_blur_v", k_blur_v<<<PixGrid(w_, h_, 6), 256, 0, s>>>(bp, w_, h_));
+    GZ_TIMED("lowfreq_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -521,14 +558,14 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
   {
     const int wc = w_ - 5, hc = h_ - 5;
-    const int st = HostTables().blur[kSigDiffmap].step;
-    const int dxc = (wc + st - 1) / st;
-    GZ_TIMED("diffmap_blur_h", k_diffmap_blur_h<<<PixGrid(dxc, hc), 256, 0, s>>>(d_resval_, rw_, wc, hc, d_tmp_));
     BlurPlanes bd{};
+    bd.out[0] = d_tmp_;
+    bd.sig[0] = kSigDiffmap;
+    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<<<BlurHGrid(wc, hc, 1, bd), 256, 0, s>>>(
+        RowsDiffmap{d_resval_, rw_}, bd, wc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    bd.sig[0] = kSigDiffmap;
-    GZ_TIMED("diffmap_blur_v", k_blur_v<<<PixGrid(dxc, hc), 256, 0, s>>>(bd, wc, hc));
+    GZ_TIMED("diffmap_blur_v", k_blur_v<<<BlurVGrid(wc, hc, 1, bd), 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,

@@ -114,6 +114,8 @@ class Engine {
   float* d_block_max_ = nullptr;
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
+  float* d_scales_ = nullptr;  // [sigma][axis][scale_stride_] border scales
+  int scale_stride_ = 0;
   // pinned host staging
   float* h_block_max_ = nullptr;
 };

@@ -68,6 +68,12 @@ def host_e2e_bin():
 
 
 @pytest.fixture(scope="session")
+def lazy_sort_check_bin():
+    """tests/native/lazy_sort_check: LazyStdSort vs libstdc++ std::sort."""
+    return _native_bin("lazy_sort_check", False)
+
+
+@pytest.fixture(scope="session")
 def writer_check_bin():
     """tests/native/writer_check: direct parallel encoder vs SaveToJpegData + WriteJpeg."""
     return _native_bin("writer_check", False)

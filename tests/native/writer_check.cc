@@ -36,7 +36,7 @@ int main(int argc, char** argv) {
     a.clear();
     gz::JpegData out = jpg;
     img.SaveToJpegData(&out);
-    gz::WriteJpeg(out, true, &a);
+    gz::WriteJpegReference(out, true, &a);
   }
   auto t1 = Clock::now();
   gz::ScanScratch* s = gz::NewScanScratch();
@@ -46,6 +46,14 @@ int main(int argc, char** argv) {
   }
   auto t2 = Clock::now();
   gz::FreeScanScratch(s);
+  // the staged path of WriteJpeg on a JpegData (3 quant tables, q=1 input)
+  std::string c, d;
+  gz::WriteJpegReference(jpg, false, &c);
+  gz::WriteJpeg(jpg, false, &d);
+  if (c != d) {
+    printf("{\"equal\": 0, \"what\": \"jpegdata\"}\n");
+    return 4;
+  }
   const double ta = std::chrono::duration<double>(t1 - t0).count() / reps;
   const double tb = std::chrono::duration<double>(t2 - t1).count() / reps;
   printf("{\"bytes\": %zu, \"equal\": %d, \"serial_ms\": %.3f, \"direct_ms\": %.3f}\n", a.size(),

@@ -95,6 +95,16 @@ def test_direct_writer_matches_serial_writer(gz, writer_check_bin, tmp_path, w, 
         assert json.loads(res.stdout)["equal"] == 1
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_lazy_sort_matches_libstdcxx_sort(lazy_sort_check_bin, seed):
+    """The prefix-on-demand sort of the search loop's change order reproduces
+    std::sort's permutation, ties included."""
+    res = subprocess.run([lazy_sort_check_bin, str(seed)], capture_output=True, text=True,
+                         timeout=300)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert json.loads(res.stdout)["bad"] == 0
+
+
 def test_synthetic_frames_deterministic(gz):
     for name, e in MANIFEST.get("synthetic", {}).items():
         if e["w"] * e["h"] > 640 * 360:
