@@ -167,9 +167,10 @@ inline dim3 BlurVGrid(int w, int h, int planes, const BlurPlanes& bp) {
   const int st = MinStep(planes, bp);
   return dim3(((w + st - 1) / st + 255) / 256, (h + st - 1) / st, planes);
 }
-inline RowsPlain Rows(const BlurPlanes& bp) {
+inline RowsPlain Rows(const BlurPlanes& bp, int w) {
   RowsPlain r{};
   for (int p = 0; p < 6; ++p) r.in[p] = bp.in[p];
+  r.w = w;
   return r;
 }
 
@@ -292,7 +293,8 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     if (!g_tab_uploaded[device]) {
       const GzTables& t = HostTables();
       for (const BlurSpec& b : t.blur)
-        if ((kBlurTile - 1) * b.step + 2 * b.radius + 1 + b.step > kBlurLds || 2 * b.radius + 1 > kMaxTaps)
+        if ((kBlurTile - 1) * b.step + 2 * b.radius + 1 + b.step > kBlurLds || 2 * b.radius + 1 > kMaxTaps ||
+            b.step < 1 || b.step > 4)
           return fail("blur spec exceeds the tiled kernel's LDS span");
       if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(t)) != hipSuccess)
         return fail("table upload failed");
@@ -400,7 +402,7 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
     bp.sig[c] = kSigOpsin;
   }
   GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
-      Rows(bp), bp, w_, d_scales_, scale_stride_));
+      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_,
                                                                       d_scales_, scale_stride_));
   GZ_HIP(hipStreamSynchronize(s));
@@ -455,7 +457,7 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
     bp.sig[c] = kSigMaskX + c;
   }
   GZ_TIMED("mask_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
-      Rows(bp), bp, w_, d_scales_, scale_stride_));
+      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
@@ -488,7 +490,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[c] = kSigOpsin;
   }
   GZ_TIMED("opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
-      Rows(bp), bp, w_, d_scales_, scale_stride_));
+      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_,
                                                                   d_scales_, scale_stride_));
   if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
@@ -507,7 +509,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     bp.sig[3 + c] = sig;
   }
   GZ_TIMED("edge_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
-      Rows(bp), bp, w_, d_scales_, scale_stride_));
+      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int p = 0; p < 6; ++p) {
     bp.in[p] = d_tmp_ + p * n;
     bp.out[p] = d_bl_ + p * n;
@@ -516,7 +518,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
-  GZ_TIMED("block_diff", k_block_diff<<<(static_cast<unsigned>(rn) + kBdPoints - 1) / kBdPoints, 256, 0, s>>>(
+  GZ_TIMED("block_diff", k_block_diff<<<(static_cast<unsigned>(rn) + 63) / 64, 64, 0, s>>>(
       d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_));
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
@@ -529,7 +531,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
   GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
-      Rows(bp), bp, w_, d_scales_, scale_stride_));
+      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
