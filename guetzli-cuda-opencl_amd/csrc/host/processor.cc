@@ -320,36 +320,79 @@ size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::ve
   return size;
 }
 
-// UpdateACHistogram (processor.cc:491-515) that also keeps raw_bits = sum_i (counts[i]/2) *
-// (depth[i] + (i & 0xf)) -- the pre-rounding term of HistogramEntropyCost --
-// current for fixed depths, so the size estimate is O(1) per change.
-void UpdateACHistogramCost(int weight, const coeff_t* coeffs, const int* q, const uint8_t* depth,
-                           JpegHistogram* h, int64_t* raw_bits) {
-  int r = 0;
-  int64_t delta = 0;
-  for (int k = 1; k < 64; ++k) {
-    const int kn = kJPEGNaturalOrder[k];
-    const coeff_t c = coeffs[kn];
-    if (c == 0) {
-      ++r;
-      continue;
-    }
-    while (r > 15) {
-      h->Add(0xf0, weight);
-      delta += depth[0xf0];
-      r -= 16;
-    }
-    const int sym = (r << 4) + Log2FloorNonZero(std::abs(c / q[kn])) + 1;  // q[kn] != 0
-    h->Add(sym, weight);
-    delta += depth[sym] + (sym & 0xf);
-    r = 0;
+// The AC histogram update of one coefficient change in the search loop
+// (UpdateACHistogram(-1, block) / change / UpdateACHistogram(+1, block),
+// processor.cc:491-515 and :869-874) done locally: in zigzag order a block's
+// AC symbols are, per non-zero coefficient, the ZRLs and run/size symbol of
+// the zero run before it, then EOB if zeros trail.  Changing the
+// coefficient at zigzag position z only re-forms the symbols of the segment
+// from the previous non-zero p to the next non-zero nx, so only those are
+// removed and re-added (same counts as the full rescans).  raw_bits tracks
+// sum_i (counts[i]/2) * (depth[i] + (i & 0xf)) -- HistogramEntropyCost
+// before rounding -- for the current depths.
+struct AcBlockModel {
+  std::vector<uint64_t> nz;  // [c * blocks + b]: bit z set <=> zigzag coefficient z non-zero
+
+  void Build(const CoeffImage& img) {
+    nz.assign(static_cast<size_t>(3) * img.blocks, 0);
+    for (int c = 0; c < 3; ++c)
+      for (int b = 0; b < img.blocks; ++b) {
+        const coeff_t* blk = img.block(c, b);
+        uint64_t m = 0;
+        for (int z = 0; z < 64; ++z) m |= static_cast<uint64_t>(blk[kJPEGNaturalOrder[z]] != 0) << z;
+        nz[static_cast<size_t>(c) * img.blocks + b] = m;
+      }
   }
-  if (r > 0) {
-    h->Add(0, weight);
-    delta += depth[0];
+
+  static int Size(coeff_t v, int q) { return Log2FloorNonZero(std::abs(v / q)) + 1; }
+
+  // weight * symbols of the segment after non-zero position p (0 = none /
+  // DC) through the non-zeros `mid` (0: none) and `nx` (0: none; then EOB
+  // if the last one is below 63).
+  static void Segment(int weight, int p, int mid, int mid_size, int nx, int nx_size,
+                      const uint8_t* depth, JpegHistogram* h, int64_t* raw) {
+    int last = p;
+    int64_t bits = 0;
+    auto put = [&](int pos, int size) {
+      int run = pos - last - 1;
+      while (run > 15) {
+        h->Add(0xf0, weight);
+        bits += depth[0xf0];
+        run -= 16;
+      }
+      const int sym = (run << 4) + size;
+      h->Add(sym, weight);
+      bits += depth[sym] + (sym & 0xf);
+      last = pos;
+    };
+    if (mid) put(mid, mid_size);
+    if (nx) {
+      put(nx, nx_size);
+    } else if (last < 63) {
+      h->Add(0, weight);
+      bits += depth[0];
+    }
+    *raw += weight * bits;
   }
-  *raw_bits += weight * delta;
-}
+
+  // block[k] := newval with the histogram / raw-bit bookkeeping.
+  void Change(int c, int bix, int blocks, coeff_t* block, int k, coeff_t newval, const int* q,
+              const uint8_t* depth, JpegHistogram* h, int64_t* raw) {
+    const coeff_t old = block[k];
+    block[k] = newval;
+    const int z = kJPEGZigZagOrder[k];
+    if (z == 0 || old == newval) return;  // DC is not an AC symbol
+    uint64_t& m = nz[static_cast<size_t>(c) * blocks + bix];
+    const uint64_t below = m & ((1ull << z) - 1) & ~1ull;
+    const uint64_t above = z < 63 ? m & ~((2ull << z) - 1) : 0;
+    const int p = below ? 63 - __builtin_clzll(below) : 0;
+    const int nx = above ? __builtin_ctzll(above) : 0;
+    const int nx_size = nx ? Size(block[kJPEGNaturalOrder[nx]], q[kJPEGNaturalOrder[nx]]) : 0;
+    Segment(-1, p, old ? z : 0, old ? Size(old, q[k]) : 0, nx, nx_size, depth, h, raw);
+    Segment(1, p, newval ? z : 0, newval ? Size(newval, q[k]) : 0, nx, nx_size, depth, h, raw);
+    if (newval) m |= 1ull << z; else m &= ~(1ull << z);
+  }
+};
 
 int64_t HistogramRawBits(const JpegHistogram& h, const uint8_t* depth) {
   int64_t bits = 0;
@@ -565,6 +608,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       raw_bits[c] = HistogramRawBits(ac_histograms[c], &ac_depths[c * JpegHistogram::kSize]);
   };
   refresh_raw();
+  AcBlockModel acm;
+  acm.Build(*img);
   int prev_size = base_size;
   std::vector<float> max_block_error(num_blocks, 0.0f);
   std::vector<int> last_indexes(num_blocks, 0);
@@ -635,6 +680,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // are those of the last i % 10 == 0 step.  Codes of decades that contain
       // no such step are never read, so they are not built.  Exact.
       const size_t n_order = global_order.size();
+      double codes_s = 0.0;
+      int n_codes = 0;
       for (size_t i = 0; i < n_order; ++i) {
         if (i >= sorter.sorted()) sorter.EnsureSorted(i);
         const int bix = global_order[i].first;
@@ -647,20 +694,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const JpegComponent& comp = jpg.components[c];
         const int jpg_bix = by * comp.width_in_blocks + bx;
         const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
-        coeff_t* block = img->block(c, bix);
-        const uint8_t* depth = &ac_depths[c * JpegHistogram::kSize];
-        UpdateACHistogramCost(-1, block, quant, depth, &ac_histograms[c], &raw_bits[c]);
-        block[k] = static_cast<coeff_t>(newval);
-        UpdateACHistogramCost(1, block, quant, depth, &ac_histograms[c], &raw_bits[c]);
+        acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
+                   &ac_depths[c * JpegHistogram::kSize], &ac_histograms[c], &raw_bits[c]);
         last_indexes[bix] += direction;
         val_threshold = global_order[i].second;
         ++changed_coeffs;
         const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
         if (i % 10 == 0 &&
             (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs_to_change)) || i + 10 >= n_order)) {
+          const auto te = Clock::now();
           ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
           refresh_raw();
-          ++res_->detail["backend_entropy_codes"];
+          codes_s += Since(te);
+          ++n_codes;
         }
         if (!needed) continue;
         est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
@@ -668,6 +714,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           break;
       }
       res_->detail["backend_changes_s"] += Since(tc);
+      res_->detail["backend_codes_s"] += codes_s;
+      res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += changed_coeffs;
       ++img->version;
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
