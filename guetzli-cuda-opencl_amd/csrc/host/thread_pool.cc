@@ -19,8 +19,10 @@ class Pool {
   }
   // Leaked at exit on purpose (workers may still be parked in wait()).
 
-  void Run(int n, const std::function<void(int)>& fn) {
-    std::lock_guard<std::mutex> serial(run_mu_);
+  // False (nothing run) if another caller holds the pool.
+  bool TryRun(int n, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> serial(run_mu_, std::try_to_lock);
+    if (!serial.owns_lock()) return false;
     {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
@@ -34,6 +36,7 @@ class Pool {
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [this] { return active_ == 0; });
     fn_ = nullptr;
+    return true;
   }
 
  private:
@@ -91,7 +94,10 @@ void ParallelFor(int n, const std::function<void(int)>& fn) {
     for (int i = 0; i < n; ++i) fn(i);
     return;
   }
-  GetPool()->Run(n, fn);
+  // Concurrent encodes (several frames per GPU) each run their passes inline
+  // when another one holds the pool, instead of queueing behind it.
+  if (!GetPool()->TryRun(n, fn))
+    for (int i = 0; i < n; ++i) fn(i);
 }
 
 }  // namespace gz

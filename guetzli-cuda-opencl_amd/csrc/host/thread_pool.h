@@ -1,8 +1,8 @@
 // Fixed-size host worker pool for the data-parallel host passes of the search
-// loop (scan encoding, histograms, candidate ordering).  One pool per process;
-// ParallelFor calls from different threads are serialised.  The worker count
+// loop (scan encoding, histograms).  One pool per process.  The worker count
 // is GZ_HOST_THREADS, else min(16, hardware threads) — 16 being the CPU share
-// a GPU gets on the target nodes.
+// a GPU gets on the target nodes.  The pool is not re-entrant; callers that
+// find it busy run their items inline (ParallelFor).
 #pragma once
 
 #include <stddef.h>
@@ -14,7 +14,8 @@ namespace gz {
 int HostThreads();
 
 // Runs fn(i) for i in [0, n) on the pool (the caller takes part) and returns
-// when all are done.  Items are handed out dynamically.
+// when all are done.  Items are handed out dynamically.  If another thread
+// is using the pool, the items run on the calling thread instead.
 void ParallelFor(int n, const std::function<void(int)>& fn);
 
 }  // namespace gz
