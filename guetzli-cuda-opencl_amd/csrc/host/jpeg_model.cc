@@ -73,6 +73,7 @@ void CoeffImage::Init(int w, int h) {
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) quant[c][k] = 1;
   ++version;
+  InvalidateLog();
 }
 
 void CoeffImage::CopyFromJpegData(const JpegData& jpg) {
@@ -88,6 +89,7 @@ void CoeffImage::CopyFromJpegData(const JpegData& jpg) {
     std::memcpy(quant[c], q, sizeof(quant[c]));
   }
   ++version;
+  InvalidateLog();
 }
 
 void CoeffImage::ApplyGlobalQuantization(const int q[3][kDCTBlockSize]) {
@@ -98,6 +100,7 @@ void CoeffImage::ApplyGlobalQuantization(const int q[3][kDCTBlockSize]) {
     std::memcpy(quant[c], q[c], sizeof(quant[c]));
   }
   ++version;
+  InvalidateLog();
 }
 
 bool CoeffImage::ComponentIsAllZero(int c) const {

@@ -61,6 +61,24 @@ struct CoeffImage {
   int quant[3][kDCTBlockSize];
   // Bumped on every host-side change so a device mirror knows when to re-upload.
   uint64_t version = 0;
+  // Flat indices of coefficients written since version `log_base` (a device
+  // mirror at that version needs only these); log_base == kNoLog after bulk
+  // rewrites.  Mutable: the device mirror resets it when it syncs.
+  static constexpr uint64_t kNoLog = ~0ull;
+  mutable std::vector<uint32_t> changed;
+  mutable uint64_t log_base = kNoLog;
+  void MarkChanged(int c, int block_ix, int k) {
+    if (log_base != kNoLog)
+      changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * blocks + block_ix) * 64 + k));
+  }
+  void InvalidateLog() const {
+    changed.clear();
+    log_base = kNoLog;
+  }
+  void ResetLog() const {  // a mirror now holds `version`
+    changed.clear();
+    log_base = version;
+  }
 
   void Init(int w, int h);
   coeff_t* block(int c, int block_ix) { return &coeffs[(static_cast<size_t>(c) * blocks + block_ix) * 64]; }

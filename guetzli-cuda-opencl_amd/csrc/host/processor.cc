@@ -19,6 +19,7 @@
 #include "host/jpeg_encode.h"
 #include "host/jpeg_writer.h"
 #include "host/lazy_sort.h"
+#include "host/thread_pool.h"
 
 namespace gz {
 
@@ -83,7 +84,8 @@ std::unique_ptr<HipButteraugliComparator> HipButteraugliComparator::Create(
 }
 
 bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
-  std::vector<coeff_t> all;
+  std::vector<coeff_t>& all = orig_;
+  all.clear();
   for (int c = 0; c < 3; ++c)
     all.insert(all.end(), jpg.components[c].coeffs.begin(), jpg.components[c].coeffs.end());
   if (!engine_->SetOriginalCoeffs(all.data(), false)) {
@@ -93,15 +95,32 @@ bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
   return true;
 }
 
+// Brings the device copy of the coefficients to img.version: the logged
+// edits only when the device holds the log's base version, else everything.
+bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
+  if (device_version_ == img.version) return true;
+  bool ok;
+  if (img.log_base != CoeffImage::kNoLog && img.log_base == device_version_ &&
+      img.changed.size() < img.coeffs.size() / 8) {
+    const size_t n = img.changed.size();
+    delta_val_.resize(n);
+    for (size_t i = 0; i < n; ++i) delta_val_[i] = img.coeffs[img.changed[i]];
+    ok = engine_->UploadCoeffDelta(img.changed.data(), delta_val_.data(), n);
+  } else {
+    ok = engine_->UploadCoeffs(img.coeffs.data());
+  }
+  if (!ok) {
+    err_ = engine_->error();
+    return false;
+  }
+  device_version_ = img.version;
+  img.ResetLog();
+  return true;
+}
+
 bool HipButteraugliComparator::Compare(const CoeffImage& img) {
   const auto t0 = Clock::now();
-  if (device_version_ != img.version) {
-    if (!engine_->UploadCoeffs(img.coeffs.data())) {
-      err_ = engine_->error();
-      return false;
-    }
-    device_version_ = img.version;
-  }
+  if (!SyncCoeffs(img)) return false;
   if (!engine_->Compare(&distance_, block_max_.data(), nullptr)) {
     err_ = engine_->error();
     return false;
@@ -112,13 +131,26 @@ bool HipButteraugliComparator::Compare(const CoeffImage& img) {
 }
 
 bool HipButteraugliComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) {
-  if (!engine_->QuantizeFromOriginal(q, img->coeffs.data())) {
+  // CopyFromJpegData(q=1) + ApplyGlobalQuantization (processor.cc:316-317)
+  // on both sides: the device quantizes its copy of the originals, the host
+  // its own (the same integer function; no 2-byte-per-coefficient download).
+  if (!engine_->QuantizeFromOriginal(q, nullptr)) {
     err_ = engine_->error();
     return false;
   }
+  const size_t per = static_cast<size_t>(img->blocks) * 64;
+  const size_t chunk = 1 << 16;
+  const int nchunks = static_cast<int>((3 * per + chunk - 1) / chunk);
+  coeff_t* dst = img->coeffs.data();
+  const coeff_t* src = orig_.data();
+  ParallelFor(nchunks, [&](int ch) {
+    const size_t b = ch * chunk, e = std::min(3 * per, b + chunk);
+    for (size_t i = b; i < e; ++i) dst[i] = QuantizeCoeff(src[i], q[i / per][i & 63]);
+  });
   for (int c = 0; c < 3; ++c) std::memcpy(img->quant[c], q[c], sizeof(img->quant[c]));
   ++img->version;
   device_version_ = img->version;
+  img->ResetLog();
   return true;
 }
 
@@ -134,13 +166,7 @@ bool HipButteraugliComparator::BlockZeroingOrders(const CoeffImage& img, const J
                                                   int comp_mask, int lookahead,
                                                   std::vector<CoeffData>* out) {
   const auto t0 = Clock::now();
-  if (device_version_ != img.version) {
-    if (!engine_->UploadCoeffs(img.coeffs.data())) {
-      err_ = engine_->error();
-      return false;
-    }
-    device_version_ = img.version;
-  }
+  if (!SyncCoeffs(img)) return false;
   out->resize(static_cast<size_t>(img.blocks) * 192);
   static_assert(sizeof(CoeffData) == sizeof(CoeffDataHost), "CoeffData layout");
   if (!engine_->BlockZeroingOrders(comp_mask, target_, lookahead,
@@ -696,6 +722,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
         acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
                    &ac_depths[c * JpegHistogram::kSize], &ac_histograms[c], &raw_bits[c]);
+        img->MarkChanged(c, bix, k);
         last_indexes[bix] += direction;
         val_threshold = global_order[i].second;
         ++changed_coeffs;

@@ -38,7 +38,8 @@ class Comparator {
   virtual void FinishBlockComparisons() = 0;
   virtual bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
                                   int lookahead, std::vector<CoeffData>* out) = 0;
-  // Device-side CopyFromJpegData(q=1) + ApplyGlobalQuantization(q); fills img.
+  // CopyFromJpegData(q=1) + ApplyGlobalQuantization(q) of the originals into img
+  // (and into any device mirror).
   virtual bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) = 0;
   virtual double ScoreOutputSize(int size) const = 0;
   virtual bool DistanceOK(double target_mul) const = 0;
@@ -92,7 +93,11 @@ class HipButteraugliComparator : public Comparator {
   int compares = 0;
 
  private:
+  bool SyncCoeffs(const CoeffImage& img);
+
   std::unique_ptr<Engine> engine_;
+  std::vector<coeff_t> orig_;      // q=1 coefficients of the original (host copy)
+  std::vector<coeff_t> delta_val_;
   int w_ = 0, h_ = 0;
   float target_ = 0.0f;
   float distance_ = 0.0f;
@@ -115,7 +120,7 @@ struct ProcessResult {
   // host-side breakdown
   double seconds_setup = 0.0;      // RGB -> q=1 coefficients, engine creation, reference upload
   double seconds_write = 0.0;      // SaveToJpegData + WriteJpeg per iteration
-  double seconds_quantize = 0.0;   // device quantization + coefficient download
+  double seconds_quantize = 0.0;   // global quantization (device copy + host copy)
   double seconds_backend = 0.0;    // SelectFrequencyBackEnd selection / size estimation
   // finer breakdown / counters (reported as JSON by gz_last_process_detail)
   std::map<std::string, double> detail;

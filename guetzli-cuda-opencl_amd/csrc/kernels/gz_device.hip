@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -383,10 +384,13 @@ Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
-                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_};
+                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
+                  d_delta_val_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h_block_max_) hipHostFree(h_block_max_);
+  if (h_delta_idx_) hipHostFree(h_delta_idx_);
+  if (h_delta_val_) hipHostFree(h_delta_val_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
 
@@ -426,6 +430,40 @@ bool Engine::UploadCoeffs(const int16_t* coeffs) {
   GZ_HIP(hipSetDevice(device_));
   GZ_HIP(hipMemcpyAsync(d_cur_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
                         hipMemcpyHostToDevice, s));
+  return true;
+}
+
+bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (n == 0) return true;
+  if (n > delta_cap_) {
+    // the previous staging buffers may still feed an in-flight copy
+    GZ_HIP(hipStreamSynchronize(s));
+    if (d_delta_idx_) GZ_HIP(hipFree(d_delta_idx_));
+    if (d_delta_val_) GZ_HIP(hipFree(d_delta_val_));
+    if (h_delta_idx_) GZ_HIP(hipHostFree(h_delta_idx_));
+    if (h_delta_val_) GZ_HIP(hipHostFree(h_delta_val_));
+    d_delta_idx_ = nullptr;
+    d_delta_val_ = nullptr;
+    h_delta_idx_ = nullptr;
+    h_delta_val_ = nullptr;
+    delta_cap_ = 0;
+    const size_t cap = std::max<size_t>(n + n / 2, 1 << 16);
+    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_delta_idx_), cap * 4));
+    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_delta_val_), cap * 2));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_idx_), cap * 4));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_val_), cap * 2));
+    delta_cap_ = cap;
+  } else {
+    // the pinned staging of the previous delta must have been consumed
+    GZ_HIP(hipStreamSynchronize(s));
+  }
+  memcpy(h_delta_idx_, idx, n * 4);
+  memcpy(h_delta_val_, val, n * 2);
+  GZ_HIP(hipMemcpyAsync(d_delta_idx_, h_delta_idx_, n * 4, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_delta_val_, h_delta_val_, n * 2, hipMemcpyHostToDevice, s));
+  GZ_TIMED("scatter_coeffs", k_scatter_coeffs<<<(n + 255) / 256, 256, 0, s>>>(d_delta_idx_, d_delta_val_, n, d_cur_));
   return true;
 }
 

@@ -55,6 +55,9 @@ class Engine {
   bool SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr);
   // Candidate coefficients ([3][blocks][64]).
   bool UploadCoeffs(const int16_t* coeffs);
+  // Applies coeffs[idx[i]] = val[i] to the device copy (stream-ordered before
+  // the next pass): the search loop's per-iteration edits, a few 10k values.
+  bool UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n);
   // cur = Quantize(orig, q) on device, copied back to host_out if non-null.
   bool QuantizeFromOriginal(const int q[3][64], int16_t* host_out);
 
@@ -115,6 +118,11 @@ class Engine {
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
   float* d_scales_ = nullptr;  // [sigma][axis][scale_stride_] border scales
+  uint32_t* d_delta_idx_ = nullptr;   // UploadCoeffDelta staging (device)
+  int16_t* d_delta_val_ = nullptr;
+  uint32_t* h_delta_idx_ = nullptr;   // ... (pinned host)
+  int16_t* h_delta_val_ = nullptr;
+  size_t delta_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
   float* h_block_max_ = nullptr;
