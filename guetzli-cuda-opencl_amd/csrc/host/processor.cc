@@ -178,6 +178,44 @@ bool HipButteraugliComparator::BlockZeroingOrders(const CoeffImage& img, const J
   return true;
 }
 
+bool Comparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg,
+                                        int comp_mask, int lookahead, std::vector<int>* offsets,
+                                        std::vector<uint8_t>* idx, std::vector<float>* err) {
+  std::vector<CoeffData> order;
+  if (!BlockZeroingOrders(img, orig_jpg, comp_mask, lookahead, &order)) return false;
+  const float limit = BlockErrorLimit();
+  offsets->assign(img.blocks + 1, 0);
+  idx->clear();
+  err->clear();
+  for (int b = 0; b < img.blocks; ++b) {
+    const CoeffData* p = &order[static_cast<size_t>(b) * 192];
+    (*offsets)[b] = static_cast<int>(idx->size());
+    for (int i = 0; i < 192; ++i) {
+      if (p[i].block_err > 0 && p[i].block_err <= limit) {
+        idx->push_back(static_cast<uint8_t>(p[i].idx));
+        err->push_back(p[i].block_err);
+      }
+    }
+  }
+  (*offsets)[img.blocks] = static_cast<int>(idx->size());
+  return true;
+}
+
+bool HipButteraugliComparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData&,
+                                                      int comp_mask, int lookahead,
+                                                      std::vector<int>* offsets,
+                                                      std::vector<uint8_t>* idx,
+                                                      std::vector<float>* err) {
+  const auto t0 = Clock::now();
+  if (!SyncCoeffs(img)) return false;
+  if (!engine_->BlockZeroingCandidates(comp_mask, target_, lookahead, offsets, idx, err)) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_zeroing += Since(t0);
+  return true;
+}
+
 double HipButteraugliComparator::ScoreOutputSize(int size) const {
   return ScoreJPEG(distance_, size, target_);
 }
@@ -571,27 +609,14 @@ bool Processor::SelectQuantMatrix(const JpegData& jpg_in, int best_q[3][kDCTBloc
 bool Processor::SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int comp_mask,
                                        double target_mul, bool stop_early, std::string* err) {
   // processor.cc:559-721 (the CPU_OPT loop runs as one batched device call)
-  const int num_blocks = img->blocks;
   if (!cmp_->StartBlockComparisons()) return Fail(err);
-  std::vector<CoeffData> order;
-  if (!cmp_->BlockZeroingOrders(*img, jpg, comp_mask, params_.zeroing_greedy_lookahead, &order))
-    return Fail(err);
-  std::vector<int> offsets(num_blocks + 1);
+  std::vector<int> offsets;
   std::vector<uint8_t> cand;
   std::vector<float> cand_err;
-  const float limit = cmp_->BlockErrorLimit();
-  for (int b = 0; b < num_blocks; ++b) {
-    const CoeffData* p = &order[static_cast<size_t>(b) * 192];
-    offsets[b] = static_cast<int>(cand.size());
-    for (int i = 0; i < 192; ++i) {
-      if (p[i].block_err > 0 && p[i].block_err <= limit) {
-        cand.push_back(static_cast<uint8_t>(p[i].idx));
-        cand_err.push_back(p[i].block_err);
-      }
-    }
-  }
+  if (!cmp_->BlockZeroingCandidates(*img, jpg, comp_mask, params_.zeroing_greedy_lookahead,
+                                    &offsets, &cand, &cand_err))
+    return Fail(err);
   cmp_->FinishBlockComparisons();
-  offsets[num_blocks] = static_cast<int>(cand.size());
   res_->detail["candidates"] = static_cast<double>(cand.size());
   return SelectFrequencyBackEnd(jpg, img, comp_mask, target_mul, stop_early, offsets, cand,
                                 cand_err, err);

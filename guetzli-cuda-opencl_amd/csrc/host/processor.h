@@ -38,6 +38,12 @@ class Comparator {
   virtual void FinishBlockComparisons() = 0;
   virtual bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
                                   int lookahead, std::vector<CoeffData>* out) = 0;
+  // The back end's input: per block the BlockZeroingOrders entries with
+  // 0 < block_err <= BlockErrorLimit(), in order, concatenated (offsets has
+  // blocks + 1 entries) -- processor.cc:690-700.  Default: filter the orders.
+  virtual bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg,
+                                      int comp_mask, int lookahead, std::vector<int>* offsets,
+                                      std::vector<uint8_t>* idx, std::vector<float>* err);
   // CopyFromJpegData(q=1) + ApplyGlobalQuantization(q) of the originals into img
   // (and into any device mirror).
   virtual bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) = 0;
@@ -75,6 +81,9 @@ class HipButteraugliComparator : public Comparator {
   void FinishBlockComparisons() override {}
   bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
                           int lookahead, std::vector<CoeffData>* out) override;
+  bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
+                              int lookahead, std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                              std::vector<float>* err) override;
   bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) override;
   double ScoreOutputSize(int size) const override;
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }

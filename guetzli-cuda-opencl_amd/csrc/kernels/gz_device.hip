@@ -340,6 +340,12 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_block_max_), e->nb_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
   alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
+  alloc(reinterpret_cast<void**>(&e->d_zero_count_), static_cast<size_t>(e->nb_) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_cand_idx_), static_cast<size_t>(e->nb_) * 192);
+  alloc(reinterpret_cast<void**>(&e->d_cand_err_), static_cast<size_t>(e->nb_) * 192 * 4);
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4) != hipSuccess)
+    ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
@@ -385,11 +391,15 @@ Engine::~Engine() {
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
-                  d_delta_val_};
+                  d_delta_val_, d_zero_count_, d_zero_off_, d_cand_idx_, d_cand_err_};
   for (void* p : bufs)
     if (p) hipFree(p);
+  if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
   if (h_block_max_) hipHostFree(h_block_max_);
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
+  if (h_zero_off_) hipHostFree(h_zero_off_);
+  if (h_cand_idx_) hipHostFree(h_cand_idx_);
+  if (h_cand_err_) hipHostFree(h_cand_err_);
   if (h_delta_val_) hipHostFree(h_delta_val_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
@@ -504,9 +514,10 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
   return true;
 }
 
-bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
+// The kernel sequence of one Compare pass (no host synchronisation);
+// captured once into a hipGraph for the plain (no debug, no profiling) case.
+bool Engine::EnqueueCompare(CompareDebug* dbg) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  GZ_HIP(hipSetDevice(device_));
   const size_t n = n_, rn = static_cast<size_t>(rw_) * rh_;
   auto d2h = [&](float* dst, const float* src, size_t count) -> bool {
     if (!dst) return true;
@@ -613,6 +624,33 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");
+  return true;
+}
+
+bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (dbg || g_prof_on.load()) {
+    if (!EnqueueCompare(dbg)) return false;
+  } else {
+    if (!compare_graph_) {
+      hipGraph_t g = nullptr;
+      GZ_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const bool ok = EnqueueCompare(nullptr);
+      const hipError_t end = hipStreamEndCapture(s, &g);
+      if (!ok) {
+        if (g) hipGraphDestroy(g);
+        return false;
+      }
+      GZ_HIP(end);
+      hipGraphExec_t exec = nullptr;
+      const hipError_t inst = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+      hipGraphDestroy(g);
+      GZ_HIP(inst);
+      compare_graph_ = exec;
+    }
+    GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(compare_graph_), s));
+  }
   GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
@@ -645,11 +683,49 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
-                                     static_cast<CoeffData*>(d_zero_out_)));
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
+  return true;
+}
+
+bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
+                                    std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                                    std::vector<float>* err) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+                                     comp_mask, limit, lookahead,
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_));
+  GZ_TIMED("scan_counts", k_scan_counts<<<1, 1024, 0, s>>>(d_zero_count_, nb_, d_zero_off_));
+  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 255) / 256, 256, 0, s>>>(
+      static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nb_, limit, d_cand_idx_, d_cand_err_));
+  GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nb_ + 1) * 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  const size_t total = static_cast<size_t>(h_zero_off_[nb_]);
+  if (total > h_cand_cap_) {
+    if (h_cand_idx_) GZ_HIP(hipHostFree(h_cand_idx_));
+    if (h_cand_err_) GZ_HIP(hipHostFree(h_cand_err_));
+    h_cand_idx_ = nullptr;
+    h_cand_err_ = nullptr;
+    h_cand_cap_ = 0;
+    const size_t cap = total + total / 4 + 1024;
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_cand_idx_), cap));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_cand_err_), cap * 4));
+    h_cand_cap_ = cap;
+  }
+  if (total) {
+    GZ_HIP(hipMemcpyAsync(h_cand_idx_, d_cand_idx_, total, hipMemcpyDeviceToHost, s));
+    GZ_HIP(hipMemcpyAsync(h_cand_err_, d_cand_err_, total * 4, hipMemcpyDeviceToHost, s));
+    GZ_HIP(hipStreamSynchronize(s));
+  }
+  ProfFlush();
+  offsets->assign(h_zero_off_, h_zero_off_ + nb_ + 1);
+  idx->assign(h_cand_idx_, h_cand_idx_ + total);
+  err->assign(h_cand_err_, h_cand_err_ + total);
   return true;
 }
 

@@ -69,6 +69,12 @@ class Engine {
   bool StartBlockComparisons(float* mask_scale_host /* 3*blocks, may be null */);
   // Per-block greedy zeroing orders for the current candidate.
   bool BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out);
+  // The same search, reduced on the device to what the back end consumes:
+  // per block the entries with 0 < block_err <= limit, in order, concatenated
+  // (offsets: blocks + 1 entries).  Moves ~5 B per kept entry instead of the
+  // 1.5 KB-per-block order table.
+  bool BlockZeroingCandidates(int comp_mask, float limit, int lookahead, std::vector<int>* offsets,
+                              std::vector<uint8_t>* idx, std::vector<float>* err);
 
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
@@ -88,6 +94,8 @@ class Engine {
   };
   std::vector<PendingEvent> pending_;
   bool MaskPipeline(const float* xyb0, const float* xyb1);
+  bool EnqueueCompare(CompareDebug* dbg);
+  void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
 
   int device_ = 0;
   int w_ = 0, h_ = 0, bw_ = 0, bh_ = 0, nb_ = 0, rw_ = 0, rh_ = 0;
@@ -117,6 +125,14 @@ class Engine {
   float* d_block_max_ = nullptr;
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
+  int* d_zero_count_ = nullptr;    // [blocks] kept entries per block
+  int* d_zero_off_ = nullptr;      // [blocks + 1] their offsets
+  uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
+  float* d_cand_err_ = nullptr;
+  int* h_zero_off_ = nullptr;      // pinned
+  uint8_t* h_cand_idx_ = nullptr;  // pinned, h_cand_cap_ entries
+  float* h_cand_err_ = nullptr;
+  size_t h_cand_cap_ = 0;
   float* d_scales_ = nullptr;  // [sigma][axis][scale_stride_] border scales
   uint32_t* d_delta_idx_ = nullptr;   // UploadCoeffDelta staging (device)
   int16_t* d_delta_val_ = nullptr;
