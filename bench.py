@@ -179,9 +179,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iters = []
+    conc = {}
+    keys = ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
+            "seconds_backend", "seconds_compare", "seconds_zeroing")
     for s in range(args.warmup, nsteps):
         sizes, stats = step(s)
         iters.extend(st.iterations for st in stats)
+        for st in stats:
+            for k in keys:
+                conc[k] = conc.get(k, 0.0) + getattr(st, k) / (args.steps * len(stats))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -270,6 +276,7 @@ def main():
         "compare_pass": compare_pass,
         "block_zeroing": {"launches": bz[0], "avg_ms": round(bz[1] / bz[0], 3)} if bz else None,
         "stages": stages,
+        "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
         "single_frame": {"seconds": round(single_s, 4),
                          "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
                          "iterations": st1.iterations,

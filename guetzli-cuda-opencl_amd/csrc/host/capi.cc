@@ -121,6 +121,13 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
   return CompareImpl(cmp, coeffs, &dbg, distance);
 }
 
+gz_status gz_comparator_original_coeffs(gz_comparator* cmp, int16_t* out) {
+  if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "original_coeffs: bad argument");
+  if (!cmp->engine->ComputeOriginalCoeffs(out))
+    return SetError(GZ_ERR_DEVICE, "original_coeffs: " + cmp->engine->error());
+  return GZ_OK;
+}
+
 gz_status gz_comparator_block_max(gz_comparator* cmp, float* out) {
   if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "block_max: bad argument");
   if (cmp->block_max.empty()) return SetError(GZ_ERR_INVALID_ARG, "block_max: no compare yet");

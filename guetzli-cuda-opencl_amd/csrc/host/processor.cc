@@ -83,7 +83,34 @@ std::unique_ptr<HipButteraugliComparator> HipButteraugliComparator::Create(
   return c;
 }
 
+bool HipButteraugliComparator::OriginalJpegData(JpegData* jpg) {
+  InitJpegDataYUV444(w_, h_, jpg);
+  for (auto& q : jpg->quant)
+    for (int k = 0; k < kDCTBlockSize; ++k) q.values[k] = 1;
+  const size_t per = static_cast<size_t>(engine_->blocks()) * 64;
+  orig_.resize(3 * per);
+  if (!engine_->ComputeOriginalCoeffs(orig_.data())) {
+    err_ = engine_->error();
+    return false;
+  }
+  for (int c = 0; c < 3; ++c)
+    std::memcpy(jpg->components[c].coeffs.data(), orig_.data() + c * per, per * sizeof(coeff_t));
+  orig_on_device_ = true;
+  return true;
+}
+
 bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
+  const size_t per = static_cast<size_t>(engine_->blocks()) * 64;
+  if (orig_on_device_ && orig_.size() == 3 * per) {
+    // already resident (OriginalJpegData) unless the caller changed them
+    bool same = true;
+    for (int c = 0; c < 3 && same; ++c)
+      same = jpg.components[c].coeffs.size() == per &&
+             std::memcmp(jpg.components[c].coeffs.data(), orig_.data() + c * per,
+                         per * sizeof(coeff_t)) == 0;
+    if (same) return true;
+  }
+  orig_on_device_ = false;
   std::vector<coeff_t>& all = orig_;
   all.clear();
   for (int c = 0; c < 3; ++c)
@@ -862,27 +889,31 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
     if (err) *err = "Could not create jpg data from rgb pixels";
     return GZ_ERR_INVALID_ARG;
   }
-  std::vector<uint8_t> host_rgb;
-  const uint8_t* hrgb = rgb;
-  if (device_ptr) {
-    host_rgb.resize(static_cast<size_t>(3) * w * h);
-    if (hipSetDevice(device) != hipSuccess ||
-        hipMemcpy(host_rgb.data(), rgb, host_rgb.size(), hipMemcpyDeviceToHost) != hipSuccess) {
-      if (err) *err = "device rgb copy failed";
-      return GZ_ERR_DEVICE;
-    }
-    hrgb = host_rgb.data();
-  }
   JpegData jpg;
-  EncodeRGBToJpegData(hrgb, w, h, &jpg);
   std::unique_ptr<HipButteraugliComparator> cmp;
   if (w >= 32 && h >= 32) {
+    // q=1 coefficients on the device from the resident reference image
     std::string e;
     cmp = HipButteraugliComparator::Create(device, w, h, rgb, device_ptr, params.butteraugli_target, &e);
-    if (!cmp) {
-      if (err) *err = e;
+    if (!cmp || !cmp->OriginalJpegData(&jpg)) {
+      if (err) *err = cmp ? cmp->error() : e;
       return GZ_ERR_DEVICE;
     }
+  } else {
+    // Below 32 px guetzli::Process skips Butteraugli and writes the q=1
+    // encode; that is the host encoder's job (no device work to mirror).
+    std::vector<uint8_t> host_rgb;
+    const uint8_t* hrgb = rgb;
+    if (device_ptr) {
+      host_rgb.resize(static_cast<size_t>(3) * w * h);
+      if (hipSetDevice(device) != hipSuccess ||
+          hipMemcpy(host_rgb.data(), rgb, host_rgb.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        if (err) *err = "device rgb copy failed";
+        return GZ_ERR_DEVICE;
+      }
+      hrgb = host_rgb.data();
+    }
+    EncodeRGBToJpegData(hrgb, w, h, &jpg);
   }
   result->seconds_setup = Since(t0);
   const int rc = ProcessJpegData(params, jpg, cmp.get(), result, err);

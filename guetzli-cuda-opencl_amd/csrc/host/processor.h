@@ -96,6 +96,9 @@ class HipButteraugliComparator : public Comparator {
                                           std::vector<float>* block_weight) override;
   const std::string& error() const override { return err_; }
   bool SetOriginalCoeffs(const JpegData& jpg) override;
+  // EncodeRGBToJpegData of the reference image, with the coefficients
+  // computed on the device (and left resident as the originals).
+  bool OriginalJpegData(JpegData* jpg);
   Engine* engine() { return engine_.get(); }
   double seconds_compare = 0.0;
   double seconds_zeroing = 0.0;
@@ -106,6 +109,7 @@ class HipButteraugliComparator : public Comparator {
 
   std::unique_ptr<Engine> engine_;
   std::vector<coeff_t> orig_;      // q=1 coefficients of the original (host copy)
+  bool orig_on_device_ = false;
   std::vector<coeff_t> delta_val_;
   int w_ = 0, h_ = 0;
   float target_ = 0.0f;

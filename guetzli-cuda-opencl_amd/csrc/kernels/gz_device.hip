@@ -346,6 +346,8 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_cand_err_), static_cast<size_t>(e->nb_) * 192 * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4) != hipSuccess)
     ok = false;
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_coeffs_), nc * sizeof(int16_t)) != hipSuccess)
+    ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
@@ -398,6 +400,7 @@ Engine::~Engine() {
   if (h_block_max_) hipHostFree(h_block_max_);
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
   if (h_zero_off_) hipHostFree(h_zero_off_);
+  if (h_coeffs_) hipHostFree(h_coeffs_);
   if (h_cand_idx_) hipHostFree(h_cand_idx_);
   if (h_cand_err_) hipHostFree(h_cand_err_);
   if (h_delta_val_) hipHostFree(h_delta_val_);
@@ -432,6 +435,18 @@ bool Engine::SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr) {
                         device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
+  return true;
+}
+
+bool Engine::ComputeOriginalCoeffs(int16_t* host_out) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  const size_t nc = static_cast<size_t>(nb_) * 64 * 3;
+  GZ_TIMED("rgb_to_coeffs", k_rgb_to_coeffs<<<(3 * nb_ + 63) / 64, 64, 0, s>>>(d_rgb_, w_, h_, bw_, nb_, d_orig_));
+  GZ_HIP(hipMemcpyAsync(h_coeffs_, d_orig_, nc * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  memcpy(host_out, h_coeffs_, nc * sizeof(int16_t));
   return true;
 }
 

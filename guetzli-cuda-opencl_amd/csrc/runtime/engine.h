@@ -53,6 +53,10 @@ class Engine {
   bool SetReference(const uint8_t* rgb, bool device_ptr);
   // q=1 coefficients of the reference ([3][blocks][64]); kept resident.
   bool SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr);
+  // EncodeRGBToJpeg's q=1 coefficients of the reference image (set by
+  // SetReference) computed on the device into the originals, and copied to
+  // host_out ([3][blocks][64]).
+  bool ComputeOriginalCoeffs(int16_t* host_out);
   // Candidate coefficients ([3][blocks][64]).
   bool UploadCoeffs(const int16_t* coeffs);
   // Applies coeffs[idx[i]] = val[i] to the device copy (stream-ordered before
@@ -129,6 +133,7 @@ class Engine {
   int* d_zero_off_ = nullptr;      // [blocks + 1] their offsets
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
+  int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
   int* h_zero_off_ = nullptr;      // pinned
   uint8_t* h_cand_idx_ = nullptr;  // pinned, h_cand_cap_ entries
   float* h_cand_err_ = nullptr;

@@ -71,6 +71,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
+    "gz_comparator_original_coeffs",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail",
 )
@@ -117,6 +118,8 @@ def lib():
     L.gz_comparator_start_block_comparisons.restype = i32
     L.gz_comparator_block_zeroing_orders.argtypes = [vp, vp, vp, i32, f32, i32, vp]
     L.gz_comparator_block_zeroing_orders.restype = i32
+    L.gz_comparator_original_coeffs.argtypes = [vp, vp]
+    L.gz_comparator_original_coeffs.restype = i32
     L.gz_synthetic_frame.argtypes = [u64, i32, i32, vp]
     L.gz_synthetic_frame.restype = i32
     L.gz_rgb_to_coeffs.argtypes = [vp, i32, i32, vp]
@@ -360,6 +363,13 @@ class ButteraugliComparator:
         _check(lib().gz_comparator_start_block_comparisons(self._h, _ptr(out)),
                "start_block_comparisons")
         return out.reshape(self.blocks, 3)
+
+    def original_coeffs(self):
+        """q=1 coefficients of the reference image, computed on the device."""
+        out = np.zeros(3 * self.blocks * 64, dtype=np.int16)
+        _check(lib().gz_comparator_original_coeffs(self._h, ctypes.c_void_p(out.ctypes.data)),
+               "original_coeffs")
+        return out
 
     def block_zeroing_orders(self, cur_coeffs, orig_coeffs, limit, comp_mask=7, lookahead=3):
         out = np.zeros(self.blocks * 192, dtype=COEFF_DTYPE)

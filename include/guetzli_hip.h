@@ -126,6 +126,11 @@ gz_status gz_comparator_compare(gz_comparator* cmp, const int16_t* coeffs, float
 /* Same, with stage dumps. */
 gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs,
                                        gz_compare_stages* stages, float* distance);
+/* EncodeRGBToJpeg's q=1 coefficients of the comparator's reference image
+ * ([3][blocks][64] int16, natural order) computed on the device: YUV16 +
+ * integer FDCT + q=1 quantizer (guetzli/jpeg_data_encoder.cc:66-136,
+ * guetzli/fdct.cc). */
+gz_status gz_comparator_original_coeffs(gz_comparator* cmp, int16_t* out);
 /* Per-8x8-block maxima of the last distance map (ceil(w/8)*ceil(h/8)). */
 gz_status gz_comparator_block_max(gz_comparator* cmp, float* out);
 /* Comparator::DistanceOK (butteraugli_comparator.h:52-54). */

@@ -86,6 +86,23 @@ def test_block_zeroing_orders_bit_exact(gz, case):
     assert bits_equal(out["block_err"], z["block_err"]), mismatch(out["block_err"], z["block_err"])
 
 
+@pytest.mark.parametrize("case", fixture_cases())
+def test_device_fdct_matches_reference(gz, case):
+    """EncodeRGBToJpeg's q=1 coefficients computed by the device kernel equal
+    the reference's (fixture orig_coeffs)."""
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    assert np.array_equal(cmp.original_coeffs(), F.i16("orig_coeffs.i16"))
+
+
+@pytest.mark.parametrize("w,h,seed", [(1920, 1080, 0), (333, 197, 8), (64, 8, 3)])
+def test_device_fdct_matches_host_encoder(gz, w, h, seed):
+    """Device FDCT == the host restatement on ragged and full-HD frames."""
+    rgb = gz.synthetic_frame(seed, w, h)
+    cmp = gz.ButteraugliComparator(w, h, rgb, 1.0)
+    assert np.array_equal(cmp.original_coeffs(), gz.rgb_to_coeffs(rgb, w, h))
+
+
 def _jpeg_sha(gz, rgb, w, h, q):
     data, stats = gz.process(rgb, w, h, gz.Params.for_quality(q), return_stats=True)
     return hashlib.sha256(data).hexdigest(), stats
