@@ -4,6 +4,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <list>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -12,6 +13,19 @@ namespace gz {
 
 namespace {
 
+// Several encodes (frames) run concurrently per process, each issuing its
+// own data-parallel passes: every ParallelFor is a job on a shared list and
+// idle workers take items from the oldest job that has some left, so
+// concurrent callers share the workers instead of queueing behind each
+// other.  The caller works on its own job too and returns when all its
+// items are done.
+struct Job {
+  const std::function<void(int)>* fn;
+  int n;
+  std::atomic<int> next{0};
+  std::atomic<int> done{0};
+};
+
 class Pool {
  public:
   explicit Pool(int workers) {
@@ -19,56 +33,74 @@ class Pool {
   }
   // Leaked at exit on purpose (workers may still be parked in wait()).
 
-  // False (nothing run) if another caller holds the pool.
-  bool TryRun(int n, const std::function<void(int)>& fn) {
-    std::unique_lock<std::mutex> serial(run_mu_, std::try_to_lock);
-    if (!serial.owns_lock()) return false;
+  void Run(int n, const std::function<void(int)>& fn) {
+    Job job;
+    job.fn = &fn;
+    job.n = n;
+    std::list<Job*>::iterator it;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_ = n;
-      next_.store(0);
-      active_ = static_cast<int>(threads_.size());
-      ++generation_;
+      it = jobs_.insert(jobs_.end(), &job);
     }
     cv_.notify_all();
-    Work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return active_ == 0; });
-    fn_ = nullptr;
-    return true;
+    Work(&job);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      jobs_.erase(it);  // no worker can pick it up any more
+    }
+    // items claimed by workers may still be running
+    std::unique_lock<std::mutex> lk(done_mu_);
+    done_cv_.wait(lk, [&] { return job.done.load() == n; });
   }
 
  private:
-  void Work() {
-    for (;;) {
-      const int i = next_.fetch_add(1);
-      if (i >= n_) break;
-      (*fn_)(i);
+  // Runs claimed item i of `job` and then further items until none is left.
+  // The next item is claimed BEFORE the current one is counted as done: the
+  // owner (who waits for done == n) keeps the job alive while this thread
+  // holds an uncounted item, and the job is not touched after the last count.
+  void Drain(Job* job, int i) {
+    const int n = job->n;
+    const std::function<void(int)>* fn = job->fn;
+    while (i < n) {
+      (*fn)(i);
+      const int next = job->next.fetch_add(1);
+      if (job->done.fetch_add(1) + 1 == n) {
+        std::lock_guard<std::mutex> lk(done_mu_);
+        done_cv_.notify_all();
+      }
+      i = next;
     }
   }
+  void Work(Job* job) { Drain(job, job->next.fetch_add(1)); }
+
   void Loop() {
-    uint64_t seen = 0;
     for (;;) {
+      Job* job = nullptr;
+      int i;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return generation_ != seen; });
-        seen = generation_;
+        cv_.wait(lk, [&] {
+          for (Job* j : jobs_)
+            if (j->next.load() < j->n) {
+              job = j;
+              return true;
+            }
+          return false;
+        });
+        // claimed under mu_: the owner erases the job under mu_ first
+        i = job->next.fetch_add(1);
+        if (i >= job->n) continue;
       }
-      Work();
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--active_ == 0) done_cv_.notify_one();
+      Drain(job, i);
     }
   }
 
   std::vector<std::thread> threads_;
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(int)>* fn_ = nullptr;
-  int n_ = 0;
-  std::atomic<int> next_{0};
-  int active_ = 0;
-  uint64_t generation_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::list<Job*> jobs_;
+  std::mutex done_mu_;
+  std::condition_variable done_cv_;
 };
 
 Pool* GetPool() {
@@ -94,10 +126,7 @@ void ParallelFor(int n, const std::function<void(int)>& fn) {
     for (int i = 0; i < n; ++i) fn(i);
     return;
   }
-  // Concurrent encodes (several frames per GPU) each run their passes inline
-  // when another one holds the pool, instead of queueing behind it.
-  if (!GetPool()->TryRun(n, fn))
-    for (int i = 0; i < n; ++i) fn(i);
+  GetPool()->Run(n, fn);
 }
 
 }  // namespace gz

@@ -74,6 +74,12 @@ def lazy_sort_check_bin():
 
 
 @pytest.fixture(scope="session")
+def pool_check_bin():
+    """tests/native/pool_check: the shared host worker pool under concurrency."""
+    return _native_bin("pool_check", False)
+
+
+@pytest.fixture(scope="session")
 def writer_check_bin():
     """tests/native/writer_check: direct parallel encoder vs SaveToJpegData + WriteJpeg."""
     return _native_bin("writer_check", False)

@@ -105,6 +105,11 @@ def test_lazy_sort_matches_libstdcxx_sort(lazy_sort_check_bin, seed):
     assert json.loads(res.stdout)["bad"] == 0
 
 
+def test_host_pool_concurrent_and_nested(pool_check_bin):
+    res = subprocess.run([pool_check_bin], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0 and res.stdout.startswith("ok"), res.stdout + res.stderr
+
+
 def test_synthetic_frames_deterministic(gz):
     for name, e in MANIFEST.get("synthetic", {}).items():
         if e["w"] * e["h"] > 640 * 360:
