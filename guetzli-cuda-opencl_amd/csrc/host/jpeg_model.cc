@@ -72,8 +72,7 @@ void CoeffImage::Init(int w, int h) {
   coeffs.assign(static_cast<size_t>(blocks) * 64 * 3, 0);
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) quant[c][k] = 1;
-  ++version;
-  InvalidateLog();
+  BulkChanged();
 }
 
 void CoeffImage::CopyFromJpegData(const JpegData& jpg) {
@@ -88,8 +87,7 @@ void CoeffImage::CopyFromJpegData(const JpegData& jpg) {
       }
     std::memcpy(quant[c], q, sizeof(quant[c]));
   }
-  ++version;
-  InvalidateLog();
+  BulkChanged();
 }
 
 void CoeffImage::ApplyGlobalQuantization(const int q[3][kDCTBlockSize]) {
@@ -99,8 +97,7 @@ void CoeffImage::ApplyGlobalQuantization(const int q[3][kDCTBlockSize]) {
     for (size_t i = 0; i < n; ++i) p[i] = QuantizeCoeff(p[i], q[c][i & 63]);
     std::memcpy(quant[c], q[c], sizeof(quant[c]));
   }
-  ++version;
-  InvalidateLog();
+  BulkChanged();
 }
 
 bool CoeffImage::ComponentIsAllZero(int c) const {

@@ -59,25 +59,18 @@ struct CoeffImage {
   int width = 0, height = 0, block_w = 0, block_h = 0, blocks = 0;
   std::vector<coeff_t> coeffs;
   int quant[3][kDCTBlockSize];
-  // Bumped on every host-side change so a device mirror knows when to re-upload.
-  uint64_t version = 0;
-  // Flat indices of coefficients written since version `log_base` (a device
-  // mirror at that version needs only these); log_base == kNoLog after bulk
-  // rewrites.  Mutable: the device mirror resets it when it syncs.
-  static constexpr uint64_t kNoLog = ~0ull;
-  mutable std::vector<uint32_t> changed;
-  mutable uint64_t log_base = kNoLog;
+  // Change journal for mirrors of the coefficients (the device copy, the
+  // writer's quantized copy): `epoch` changes on every bulk rewrite, within
+  // an epoch every single-coefficient write appends its flat index to
+  // `changed`.  A mirror remembers the (epoch, journal length) it reflects.
+  uint64_t epoch = 0;
+  std::vector<uint32_t> changed;
   void MarkChanged(int c, int block_ix, int k) {
-    if (log_base != kNoLog)
-      changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * blocks + block_ix) * 64 + k));
+    changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * blocks + block_ix) * 64 + k));
   }
-  void InvalidateLog() const {
+  void BulkChanged() {
+    ++epoch;
     changed.clear();
-    log_base = kNoLog;
-  }
-  void ResetLog() const {  // a mirror now holds `version`
-    changed.clear();
-    log_base = version;
   }
 
   void Init(int w, int h);
@@ -95,6 +88,18 @@ struct CoeffImage {
   // for a component count already known.
   void SaveHeaderToJpegData(int ncomp, JpegData* jpg) const;
   bool ComponentIsAllZero(int c) const;
+};
+
+// What a mirror of a CoeffImage reflects (see CoeffImage::epoch).
+struct CoeffCursor {
+  uint64_t epoch = ~0ull;
+  size_t pos = 0;
+  bool Current(const CoeffImage& img) const { return epoch == img.epoch && pos == img.changed.size(); }
+  bool CanReplay(const CoeffImage& img) const { return epoch == img.epoch && pos <= img.changed.size(); }
+  void Set(const CoeffImage& img) {
+    epoch = img.epoch;
+    pos = img.changed.size();
+  }
 };
 
 // Quantize (guetzli/quantize.h:25-30)

@@ -6,6 +6,8 @@
 
 #include "host/thread_pool.h"
 
+#include <emmintrin.h>
+
 namespace gz {
 
 namespace {
@@ -438,6 +440,49 @@ inline void EncodeBlock(Sink& bw, const At& at, coeff_t* last_dc, const HuffTabl
   if (r > 0) bw.Put(act.depth[0], static_cast<uint64_t>(act.code[0]));
 }
 
+// EncodeBlock for a zigzag block with its non-zero mask: the same symbols,
+// visiting only the non-zero coefficients.
+template <class Sink>
+inline void EncodeBlockMasked(Sink& bw, const coeff_t* zz, uint64_t mask, coeff_t* last_dc,
+                              const HuffTable& dct, const HuffTable& act) {
+  const coeff_t dc = zz[0];
+  coeff_t diff = static_cast<coeff_t>(dc - *last_dc);
+  *last_dc = dc;
+  coeff_t bits = diff;
+  if (diff < 0) {
+    diff = static_cast<coeff_t>(-diff);
+    --bits;
+  }
+  const int nb = Log2Floor(static_cast<uint32_t>(static_cast<int>(diff))) + 1;
+  bw.Put(dct.depth[nb], static_cast<uint64_t>(dct.code[nb]));
+  if (nb > 0) bw.Put(nb, static_cast<uint64_t>(bits & ((1 << nb) - 1)));
+  uint64_t m = mask & ~1ull;
+  int last = 0;
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    int r = k - last - 1;
+    coeff_t v = zz[k];
+    coeff_t vb;
+    if (v < 0) {
+      v = static_cast<coeff_t>(-v);
+      vb = static_cast<coeff_t>(~v);
+    } else {
+      vb = v;
+    }
+    while (r > 15) {
+      bw.Put(act.depth[0xf0], static_cast<uint64_t>(act.code[0xf0]));
+      r -= 16;
+    }
+    const int nbits = Log2FloorNonZero(static_cast<uint32_t>(static_cast<int>(v))) + 1;
+    const int sym = (r << 4) + nbits;
+    bw.Put(act.depth[sym], static_cast<uint64_t>(act.code[sym]));
+    bw.Put(nbits, static_cast<uint64_t>(vb & ((1 << nbits) - 1)));
+    last = k;
+    m &= m - 1;
+  }
+  if (last < 63) bw.Put(act.depth[0], static_cast<uint64_t>(act.code[0]));
+}
+
 // Unstuffed MSB-first bit buffer: chunks of the scan are encoded into these
 // in parallel and concatenated afterwards.
 struct RawBits {
@@ -497,21 +542,37 @@ void EmitStuffed(const std::vector<RawBits>& parts, int nparts, std::string* out
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Staged, multithreaded encode.  Stage: quantize into zigzag order and count
-// DC / AC symbols per chunk of blocks (parallel).  Encode: cluster + Huffman
-// tables (serial, tiny), scan chunks into raw bit buffers (parallel), then
-// concatenate + pad + 0xff-stuff (serial, ~bytes of output).  Only for the
-// one-block-per-MCU (4:4:4) layout; anything else takes the serial writer.
+// Staged, multithreaded encode (one-block-per-MCU, i.e. 4:4:4, layouts; any
+// other layout takes the serial writer).
+//
+// Stage: the quantized coefficients in zigzag order, a non-zero bit mask per
+// block and the DC / AC symbol histograms.  A full stage runs over chunks of
+// blocks on the pool; for a CoeffImage the stage is kept between calls and
+// later brought up to date from the image's change journal -- the search
+// loop edits a few 10k of millions of coefficients per iteration, so only
+// the touched blocks are re-quantized and their symbols swapped in the
+// histograms (histograms are counts: the result equals a full recount).
+//
+// Encode: cluster + Huffman tables (serial, tiny), scan chunks into raw bit
+// buffers (parallel), then concatenate + pad + 0xff-stuff (serial, bytes of
+// output).
 // ---------------------------------------------------------------------------
 
 struct ScanScratch {
-  int blocks = 0, ncomp = 0, chunks = 0, per_chunk = 0;
-  std::vector<coeff_t> zz;  // [4][blocks][64] quantized, zigzag order
+  int blocks = 0, stored = 0, ncomp = 0, chunks = 0, per_chunk = 0;
+  std::vector<coeff_t> zz;        // [stored][blocks][64] quantized, zigzag order
+  std::vector<uint64_t> mask;     // [stored][blocks] bit k <=> zz[k] != 0
+  std::vector<uint8_t> stored_nz; // [stored][blocks] non-zero pre-division coefficients
+  int64_t chroma_nz = 0;          // sum of stored_nz over components 1..2
   std::vector<RawBits> parts;
-  std::vector<JpegHistogram> dc, ac;  // [chunk][4]
-  std::vector<uint8_t> nonzero;       // [chunk]: some chroma coefficient non-zero
+  std::vector<JpegHistogram> dc, ac;  // [chunk][4] during a full stage
+  std::vector<int64_t> chunk_nz;      // [chunk] chroma non-zeros during a full stage
+  JpegHistogram dc_all[4], ac_all[4]; // totals per stored component
   JpegData hdr;                       // the staged image without coefficients
-  JpegHistogram dc_h[4], ac_h[4];
+  CoeffCursor cursor;                 // CoeffImage state the stage reflects
+  std::vector<uint32_t> stamp;        // [stored * blocks] touched-block marks
+  uint32_t stamp_id = 0;
+  std::vector<uint32_t> touched;
 };
 
 ScanScratch* NewScanScratch() { return new ScanScratch; }
@@ -519,23 +580,63 @@ void FreeScanScratch(ScanScratch* s) { delete s; }
 
 namespace {
 
-// load(c, b, zz) writes block b of component c in zigzag order and returns
-// non-zero iff the stored (pre-division) block has a non-zero coefficient.
-template <class Load>
-void StageBlocks(int blocks, int ncomp, ScanScratch* s, const Load& load) {
-  s->blocks = blocks;
-  s->zz.resize(static_cast<size_t>(blocks) * 64 * ncomp);
+inline uint64_t NonzeroMask(const coeff_t* zz) {
+  uint64_t m = 0;
+  const __m128i zero = _mm_setzero_si128();
+  for (int i = 0; i < 4; ++i) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(zz + 16 * i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(zz + 16 * i + 8));
+    const __m128i z = _mm_packs_epi16(_mm_cmpeq_epi16(a, zero), _mm_cmpeq_epi16(b, zero));
+    m |= static_cast<uint64_t>(static_cast<uint16_t>(~_mm_movemask_epi8(z))) << (16 * i);
+  }
+  return m;
+}
+
+// The AC symbols of a block (processor.cc:491-515 / jpeg_data_writer.cc
+// BuildACHistograms) from its zigzag values and non-zero mask.
+inline void AddAcSymbols(const coeff_t* zz, uint64_t mask, int weight, JpegHistogram* h) {
+  uint64_t m = mask & ~1ull;
+  int last = 0;
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    int r = k - last - 1;
+    while (r > 15) {
+      h->Add(0xf0, weight);
+      r -= 16;
+    }
+    h->Add((r << 4) + Log2FloorNonZero(std::abs(zz[k])) + 1, weight);
+    last = k;
+    m &= m - 1;
+  }
+  if (last < 63) h->Add(0, weight);
+}
+
+inline int DcSymbol(coeff_t dc, coeff_t last) { return Log2Floor(std::abs(dc - last)) + 1; }
+
+void Partition(int blocks, ScanScratch* s) {
   const int target_chunks = 4 * HostThreads();
   s->per_chunk = std::max(64, (blocks + target_chunks - 1) / target_chunks);
   s->chunks = (blocks + s->per_chunk - 1) / s->per_chunk;
+}
+
+// Full stage.  load(c, b, zz) writes block b of component c in zigzag order
+// and returns the number of non-zero stored (pre-division) coefficients.
+template <class Load>
+void StageAll(int blocks, int stored, ScanScratch* s, const Load& load) {
+  s->blocks = blocks;
+  s->stored = stored;
+  s->zz.resize(static_cast<size_t>(blocks) * 64 * stored);
+  s->mask.resize(static_cast<size_t>(blocks) * stored);
+  s->stored_nz.resize(static_cast<size_t>(blocks) * stored);
+  Partition(blocks, s);
   s->dc.assign(static_cast<size_t>(s->chunks) * 4, JpegHistogram());
   s->ac.assign(static_cast<size_t>(s->chunks) * 4, JpegHistogram());
-  s->nonzero.assign(s->chunks, 0);
+  s->chunk_nz.assign(s->chunks, 0);
   ParallelFor(s->chunks, [&](int ch) {
     const int b0 = ch * s->per_chunk, b1 = std::min(blocks, b0 + s->per_chunk);
-    bool nz = false;
+    int64_t nz = 0;
     coeff_t prev[64];
-    for (int c = 0; c < ncomp; ++c) {
+    for (int c = 0; c < stored; ++c) {
       JpegHistogram& hdc = s->dc[ch * 4 + c];
       JpegHistogram& hac = s->ac[ch * 4 + c];
       coeff_t last = 0;
@@ -544,39 +645,96 @@ void StageBlocks(int blocks, int ncomp, ScanScratch* s, const Load& load) {
         last = prev[0];
       }
       for (int b = b0; b < b1; ++b) {
-        coeff_t* dst = &s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
-        if (load(c, b, dst) && c > 0) nz = true;
-        hdc.Add(Log2Floor(std::abs(dst[0] - last)) + 1);
+        const size_t bi = static_cast<size_t>(c) * blocks + b;
+        coeff_t* dst = &s->zz[bi * 64];
+        const int snz = load(c, b, dst);
+        s->stored_nz[bi] = static_cast<uint8_t>(snz);
+        if (c > 0) nz += snz;
+        const uint64_t m = NonzeroMask(dst);
+        s->mask[bi] = m;
+        hdc.Add(DcSymbol(dst[0], last));
         last = dst[0];
-        int r = 0;
-        for (int k = 1; k < 64; ++k) {
-          const coeff_t v = dst[k];
-          if (v == 0) {
-            ++r;
-            continue;
-          }
-          while (r > 15) {
-            hac.Add(0xf0);
-            r -= 16;
-          }
-          hac.Add((r << 4) + Log2FloorNonZero(std::abs(v)) + 1);
-          r = 0;
-        }
-        if (r > 0) hac.Add(0);
+        AddAcSymbols(dst, m, 1, &hac);
       }
     }
-    s->nonzero[ch] = nz;
+    s->chunk_nz[ch] = nz;
   });
+  s->chroma_nz = 0;
+  for (int ch = 0; ch < s->chunks; ++ch) s->chroma_nz += s->chunk_nz[ch];
+  for (int c = 0; c < 4; ++c) {
+    s->dc_all[c].Clear();
+    s->ac_all[c].Clear();
+    if (c >= stored) continue;
+    for (int ch = 0; ch < s->chunks; ++ch) {
+      s->dc_all[c].AddHistogram(s->dc[ch * 4 + c]);
+      s->ac_all[c].AddHistogram(s->ac[ch * 4 + c]);
+    }
+  }
+  s->stamp.assign(static_cast<size_t>(blocks) * stored, 0);
+  s->stamp_id = 0;
 }
 
-void SumHistograms(ScanScratch* s) {
-  for (int c = 0; c < 4; ++c) {
-    s->dc_h[c].Clear();
-    s->ac_h[c].Clear();
-    if (c >= s->ncomp) continue;
-    for (int ch = 0; ch < s->chunks; ++ch) {
-      s->dc_h[c].AddHistogram(s->dc[ch * 4 + c]);
-      s->ac_h[c].AddHistogram(s->ac[ch * 4 + c]);
+// Quantization as SaveToJpegData divides (output_image.cc:618-626).
+// |stored| <= 2^15 and q < 2^24: the correctly rounded f32 quotient
+// truncates to the exact integer quotient (an inexact quotient is at least
+// 1/q from an integer, the rounding error below 2^-9/q; checked exhaustively
+// for q < 2^16).
+struct CoeffImageLoader {
+  const CoeffImage& img;
+  float qz[3][64];
+  explicit CoeffImageLoader(const CoeffImage& im) : img(im) {
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 64; ++k) qz[c][k] = static_cast<float>(img.quant[c][kJPEGNaturalOrder[k]]);
+  }
+  int operator()(int c, int b, coeff_t* dst) const {
+    const coeff_t* src = img.block(c, b);
+    int nz = 0;
+    for (int k = 0; k < 64; ++k) {
+      const coeff_t v = src[kJPEGNaturalOrder[k]];
+      dst[k] = static_cast<coeff_t>(static_cast<int>(static_cast<float>(v) / qz[c][k]));
+      nz += v != 0;
+    }
+    return nz;
+  }
+};
+
+// Brings a CoeffImage stage up to date from the image's change journal.
+void StageIncremental(const CoeffImage& img, ScanScratch* s) {
+  const CoeffImageLoader load(img);
+  const int blocks = s->blocks;
+  if (++s->stamp_id == 0) {
+    std::fill(s->stamp.begin(), s->stamp.end(), 0);
+    s->stamp_id = 1;
+  }
+  s->touched.clear();
+  for (size_t i = s->cursor.pos; i < img.changed.size(); ++i) {
+    const uint32_t bi = img.changed[i] >> 6;  // c * blocks + b
+    if (s->stamp[bi] != s->stamp_id) {
+      s->stamp[bi] = s->stamp_id;
+      s->touched.push_back(bi);
+    }
+  }
+  bool dc_moved[3] = {false, false, false};
+  for (uint32_t bi : s->touched) {
+    const int c = static_cast<int>(bi / blocks), b = static_cast<int>(bi % blocks);
+    coeff_t* zz = &s->zz[static_cast<size_t>(bi) * 64];
+    AddAcSymbols(zz, s->mask[bi], -1, &s->ac_all[c]);
+    const coeff_t old_dc = zz[0];
+    const int snz = load(c, b, zz);
+    if (c > 0) s->chroma_nz += snz - s->stored_nz[bi];
+    s->stored_nz[bi] = static_cast<uint8_t>(snz);
+    s->mask[bi] = NonzeroMask(zz);
+    AddAcSymbols(zz, s->mask[bi], 1, &s->ac_all[c]);
+    if (zz[0] != old_dc) dc_moved[c] = true;
+  }
+  for (int c = 0; c < 3; ++c) {
+    if (!dc_moved[c]) continue;  // the search loop never edits DC; recount if it did
+    s->dc_all[c].Clear();
+    coeff_t last = 0;
+    for (int b = 0; b < blocks; ++b) {
+      const coeff_t dc = s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
+      s->dc_all[c].Add(DcSymbol(dc, last));
+      last = dc;
     }
   }
 }
@@ -626,28 +784,15 @@ bool WriteJpegSerial(const JpegData& jpg, bool strip_metadata, std::string* out)
 }  // namespace
 
 int StageCoeffImage(const CoeffImage& img, const JpegData& meta, ScanScratch* s) {
-  // Quantization as SaveToJpegData divides (output_image.cc:618-626).
-  // |stored| <= 2^15 and q < 2^24: the correctly rounded f32 quotient
-  // truncates to the exact integer quotient (an inexact quotient is at least
-  // 1/q from an integer, the rounding error below 2^-9/q; checked
-  // exhaustively for q < 2^16).
-  float qz[3][64];
-  for (int c = 0; c < 3; ++c)
-    for (int k = 0; k < 64; ++k) qz[c][k] = static_cast<float>(img.quant[c][kJPEGNaturalOrder[k]]);
-  StageBlocks(img.blocks, 3, s, [&](int c, int b, coeff_t* dst) {
-    const coeff_t* src = img.block(c, b);
-    int any = 0;
-    for (int k = 0; k < 64; ++k) {
-      dst[k] = static_cast<coeff_t>(
-          static_cast<int>(static_cast<float>(src[kJPEGNaturalOrder[k]]) / qz[c][k]));
-      any |= src[k];
-    }
-    return any != 0;
-  });
-  bool chroma = false;
-  for (int ch = 0; ch < s->chunks; ++ch) chroma |= s->nonzero[ch] != 0;
-  s->ncomp = chroma ? 3 : 1;  // SaveToJpegData drops all-zero chroma
-  SumHistograms(s);
+  const bool replay = s->stored == 3 && s->blocks == img.blocks && s->cursor.CanReplay(img) &&
+                      img.changed.size() - s->cursor.pos < static_cast<size_t>(img.blocks) * 8;
+  if (replay) {
+    StageIncremental(img, s);
+  } else {
+    StageAll(img.blocks, 3, s, CoeffImageLoader(img));
+  }
+  s->cursor.Set(img);
+  s->ncomp = s->chroma_nz > 0 ? 3 : 1;  // SaveToJpegData drops all-zero chroma
   s->hdr.app_data = meta.app_data;
   s->hdr.com_data = meta.com_data;
   img.SaveHeaderToJpegData(s->ncomp, &s->hdr);
@@ -661,11 +806,12 @@ bool EncodeStaged(ScanScratch* s, bool strip_metadata, std::string* out) {
   HuffTable dc_tab[4], ac_tab[4];
   JpegHistogram dc_h[4], ac_h[4];
   for (int c = 0; c < ncomps; ++c) {
-    dc_h[c] = s->dc_h[c];
-    ac_h[c] = s->ac_h[c];
+    dc_h[c] = s->dc_all[c];
+    ac_h[c] = s->ac_all[c];
   }
   WriteHuffmanSegments(hdr, dc_h, ac_h, dc_tab, ac_tab, out);
   const int blocks = s->blocks;
+  Partition(blocks, s);
   s->parts.resize(s->chunks);
   ParallelFor(s->chunks, [&](int ch) {
     RawBits& bw = s->parts[ch];
@@ -676,8 +822,8 @@ bool EncodeStaged(ScanScratch* s, bool strip_metadata, std::string* out) {
       last_dc[c] = b0 > 0 ? s->zz[(static_cast<size_t>(c) * blocks + b0 - 1) * 64] : 0;
     for (int b = b0; b < b1; ++b)
       for (int c = 0; c < ncomps; ++c) {
-        const coeff_t* zz = &s->zz[(static_cast<size_t>(c) * blocks + b) * 64];
-        EncodeBlock(bw, [zz](int k) { return zz[k]; }, &last_dc[c], dc_tab[c], ac_tab[c]);
+        const size_t bi = static_cast<size_t>(c) * blocks + b;
+        EncodeBlockMasked(bw, &s->zz[bi * 64], s->mask[bi], &last_dc[c], dc_tab[c], ac_tab[c]);
       }
   });
   EmitStuffed(s->parts, s->chunks, out);
@@ -690,8 +836,12 @@ int CoeffImageHistograms(const CoeffImage& img, ScanScratch* s, JpegHistogram dc
   JpegData none;
   const int n = StageCoeffImage(img, none, s);
   for (int c = 0; c < 3; ++c) {
-    dc[c] = s->dc_h[c];
-    ac[c] = s->ac_h[c];
+    dc[c].Clear();
+    ac[c].Clear();
+    if (c < n) {
+      dc[c] = s->dc_all[c];
+      ac[c] = s->ac_all[c];
+    }
   }
   return n;
 }
@@ -707,13 +857,12 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
   if (!IsOneBlockPerMcu(jpg)) return WriteJpegSerial(jpg, strip_metadata, out);
   ScanScratch s;
   const int ncomp = static_cast<int>(jpg.components.size());
-  StageBlocks(jpg.mcu_cols * jpg.mcu_rows, ncomp, &s, [&](int c, int b, coeff_t* dst) {
+  StageAll(jpg.mcu_cols * jpg.mcu_rows, ncomp, &s, [&](int c, int b, coeff_t* dst) {
     const coeff_t* src = &jpg.components[c].coeffs[static_cast<size_t>(b) * 64];
     for (int k = 0; k < 64; ++k) dst[k] = src[kJPEGNaturalOrder[k]];
-    return true;
+    return 0;
   });
   s.ncomp = ncomp;
-  SumHistograms(&s);
   s.hdr.width = jpg.width;
   s.hdr.height = jpg.height;
   s.hdr.mcu_cols = jpg.mcu_cols;

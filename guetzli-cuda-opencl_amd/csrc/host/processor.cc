@@ -122,17 +122,17 @@ bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
   return true;
 }
 
-// Brings the device copy of the coefficients to img.version: the logged
-// edits only when the device holds the log's base version, else everything.
+// Brings the device copy of the coefficients up to date with img: the
+// journalled edits when it is in img's epoch, else everything.
 bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
-  if (device_version_ == img.version) return true;
+  if (device_.Current(img)) return true;
   bool ok;
-  if (img.log_base != CoeffImage::kNoLog && img.log_base == device_version_ &&
-      img.changed.size() < img.coeffs.size() / 8) {
-    const size_t n = img.changed.size();
+  if (device_.CanReplay(img) && img.changed.size() - device_.pos < img.coeffs.size() / 8) {
+    const size_t n = img.changed.size() - device_.pos;
+    const uint32_t* idx = img.changed.data() + device_.pos;
     delta_val_.resize(n);
-    for (size_t i = 0; i < n; ++i) delta_val_[i] = img.coeffs[img.changed[i]];
-    ok = engine_->UploadCoeffDelta(img.changed.data(), delta_val_.data(), n);
+    for (size_t i = 0; i < n; ++i) delta_val_[i] = img.coeffs[idx[i]];
+    ok = engine_->UploadCoeffDelta(idx, delta_val_.data(), n);
   } else {
     ok = engine_->UploadCoeffs(img.coeffs.data());
   }
@@ -140,8 +140,7 @@ bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
     err_ = engine_->error();
     return false;
   }
-  device_version_ = img.version;
-  img.ResetLog();
+  device_.Set(img);
   return true;
 }
 
@@ -175,9 +174,8 @@ bool HipButteraugliComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize
     for (size_t i = b; i < e; ++i) dst[i] = QuantizeCoeff(src[i], q[i / per][i & 63]);
   });
   for (int c = 0; c < 3; ++c) std::memcpy(img->quant[c], q[c], sizeof(img->quant[c]));
-  ++img->version;
-  device_version_ = img->version;
-  img->ResetLog();
+  img->BulkChanged();
+  device_.Set(*img);
   return true;
 }
 
@@ -796,7 +794,6 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       res_->detail["backend_codes_s"] += codes_s;
       res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += changed_coeffs;
-      ++img->version;
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;

@@ -115,7 +115,7 @@ class HipButteraugliComparator : public Comparator {
   float target_ = 0.0f;
   float distance_ = 0.0f;
   std::vector<float> block_max_;
-  uint64_t device_version_ = ~0ull;  // CoeffImage::version mirrored on device
+  CoeffCursor device_;  // what the device copy of the coefficients reflects
   std::string err_;
 };
 

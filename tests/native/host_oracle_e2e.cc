@@ -63,7 +63,7 @@ class OracleComparator : public gz::Comparator {
       for (size_t i = 0; i < per; ++i)
         img->coeffs[c * per + i] = gz::QuantizeCoeff(orig_[c * per + i], q[c][i & 63]);
     for (int c = 0; c < 3; ++c) std::memcpy(img->quant[c], q[c], sizeof(img->quant[c]));
-    ++img->version;
+    img->BulkChanged();
     return true;
   }
   double ScoreOutputSize(int size) const override { return gz::ScoreJPEG(distance_, size, target_); }
