@@ -714,18 +714,42 @@ void StageIncremental(const CoeffImage& img, ScanScratch* s) {
       s->touched.push_back(bi);
     }
   }
+  // touched blocks in parallel chunks, each with its own histogram deltas
+  // (uint32 counts wrap, so negative deltas sum exactly)
+  const int nt = static_cast<int>(s->touched.size());
+  const int per = 256;
+  const int nchunks = (nt + per - 1) / per;
+  struct Delta {
+    JpegHistogram ac[3];
+    int64_t chroma_nz = 0;
+    bool dc_moved[3] = {false, false, false};
+  };
+  std::vector<Delta> deltas(nchunks);
+  ParallelFor(nchunks, [&](int ch) {
+    Delta& d = deltas[ch];
+    for (int c = 0; c < 3; ++c) std::memset(d.ac[c].counts, 0, sizeof(d.ac[c].counts));
+    const int t1 = std::min(nt, (ch + 1) * per);
+    for (int t = ch * per; t < t1; ++t) {
+      const uint32_t bi = s->touched[t];
+      const int c = static_cast<int>(bi / blocks), b = static_cast<int>(bi % blocks);
+      coeff_t* zz = &s->zz[static_cast<size_t>(bi) * 64];
+      AddAcSymbols(zz, s->mask[bi], -1, &d.ac[c]);
+      const coeff_t old_dc = zz[0];
+      const int snz = load(c, b, zz);
+      if (c > 0) d.chroma_nz += snz - s->stored_nz[bi];
+      s->stored_nz[bi] = static_cast<uint8_t>(snz);
+      s->mask[bi] = NonzeroMask(zz);
+      AddAcSymbols(zz, s->mask[bi], 1, &d.ac[c]);
+      if (zz[0] != old_dc) d.dc_moved[c] = true;
+    }
+  });
   bool dc_moved[3] = {false, false, false};
-  for (uint32_t bi : s->touched) {
-    const int c = static_cast<int>(bi / blocks), b = static_cast<int>(bi % blocks);
-    coeff_t* zz = &s->zz[static_cast<size_t>(bi) * 64];
-    AddAcSymbols(zz, s->mask[bi], -1, &s->ac_all[c]);
-    const coeff_t old_dc = zz[0];
-    const int snz = load(c, b, zz);
-    if (c > 0) s->chroma_nz += snz - s->stored_nz[bi];
-    s->stored_nz[bi] = static_cast<uint8_t>(snz);
-    s->mask[bi] = NonzeroMask(zz);
-    AddAcSymbols(zz, s->mask[bi], 1, &s->ac_all[c]);
-    if (zz[0] != old_dc) dc_moved[c] = true;
+  for (const Delta& d : deltas) {
+    for (int c = 0; c < 3; ++c) {
+      for (int i = 0; i + 1 < JpegHistogram::kSize; ++i) s->ac_all[c].counts[i] += d.ac[c].counts[i];
+      dc_moved[c] = dc_moved[c] || d.dc_moved[c];
+    }
+    s->chroma_nz += d.chroma_nz;
   }
   for (int c = 0; c < 3; ++c) {
     if (!dc_moved[c]) continue;  // the search loop never edits DC; recount if it did
