@@ -418,7 +418,7 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<kBlurRefOpsin><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_,
                                                                       d_scales_, scale_stride_));
@@ -519,13 +519,13 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigMaskX + c;
   }
-  GZ_TIMED("mask_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  GZ_TIMED("mask_blur_h", k_blur_h_tiled<kBlurMask><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  GZ_TIMED("mask_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 3, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  GZ_TIMED("mask_blur_v", k_blur_v<kBlurMask><<<BlurVGrid(w_, h_, 3, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -553,7 +553,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.out[c] = d_tmp_ + c * n;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<kBlurOpsin><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_,
                                                                   d_scales_, scale_stride_));
@@ -572,13 +572,13 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.sig[c] = sig;
     bp.sig[3 + c] = sig;
   }
-  GZ_TIMED("edge_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+  GZ_TIMED("edge_blur_h", k_blur_h_tiled<kBlurEdge><<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int p = 0; p < 6; ++p) {
     bp.in[p] = d_tmp_ + p * n;
     bp.out[p] = d_bl_ + p * n;
   }
-  GZ_TIMED("edge_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  GZ_TIMED("edge_blur_v", k_blur_v<kBlurEdge><<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
@@ -594,7 +594,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.sig[3 + c] = kSigLowFreq;
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<kBlurLowFreq><<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
@@ -603,7 +603,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    GZ_TIMED("lowfreq_blur_v", k_blur_v<<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    GZ_TIMED("lowfreq_blur_v", k_blur_v<kBlurLowFreq><<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -627,11 +627,11 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     BlurPlanes bd{};
     bd.out[0] = d_tmp_;
     bd.sig[0] = kSigDiffmap;
-    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<<<BlurHGrid(wc, hc, 1, bd), 256, 0, s>>>(
+    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<kBlurDiffmap><<<BlurHGrid(wc, hc, 1, bd), 256, 0, s>>>(
         RowsDiffmap{d_resval_, rw_}, bd, wc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    GZ_TIMED("diffmap_blur_v", k_blur_v<<<BlurVGrid(wc, hc, 1, bd), 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
+    GZ_TIMED("diffmap_blur_v", k_blur_v<kBlurDiffmap><<<BlurVGrid(wc, hc, 1, bd), 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
