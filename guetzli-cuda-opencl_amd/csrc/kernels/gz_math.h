@@ -62,6 +62,27 @@ struct BlurPlanes {
 extern __constant__ GzTables c_tab;
 
 // ---------------------------------------------------------------------------
+// XCD-aware workgroup numbering.  Workgroups are dealt round-robin over the
+// 8 XCDs, each with its own 4 MiB L2; renumbering them so that every XCD
+// owns one contiguous range of the (x fastest, then y, then z) grid puts the
+// neighbouring rows a stencil re-reads on the same L2.  Bijective for any
+// grid size (MI355X guide, T1).  A speed choice only: results do not depend
+// on placement.
+// ---------------------------------------------------------------------------
+struct BlockId {
+  int x, y, z;
+};
+__device__ __forceinline__ BlockId xcd_block_id() {
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned n = gx * gy * gridDim.z;
+  const unsigned lin = (blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x;
+  const unsigned q = n / 8, r = n % 8, xcd = lin % 8, k = lin / 8;
+  const unsigned id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  return BlockId{static_cast<int>(id % gx), static_cast<int>((id / gx) % gy),
+                 static_cast<int>(id / (gx * gy))};
+}
+
+// ---------------------------------------------------------------------------
 // Small helpers
 // ---------------------------------------------------------------------------
 
