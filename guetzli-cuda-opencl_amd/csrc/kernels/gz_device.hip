@@ -153,21 +153,22 @@ inline dim3 PixGrid(int w, int h, int planes = 1) {
   return dim3((w + 255) / 256, h, planes);
 }
 
-// Grids sized to the down-sampled outputs of the planes' blurs (the finest
-// step among them decides).
-int MinStep(int planes, const BlurPlanes& bp) {
-  int st = 1 << 20;
-  for (int p = 0; p < planes; ++p) st = std::min(st, HostTables().blur[bp.sig[p]].step);
-  return st;
+// Packs the planes' (tile, row) work items of a blur pass into one 1-D grid
+// (planes of different steps have different output sizes; no idle groups).
+inline dim3 PackBlurGrid(BlurPlanes* bp, int planes, int w, int h, bool vertical) {
+  bp->nplanes = planes;
+  bp->start[0] = 0;
+  for (int p = 0; p < planes; ++p) {
+    const int st = HostTables().blur[bp->sig[p]].step;
+    const int dx = (w + st - 1) / st;
+    bp->tiles[p] = (dx + 255) / 256;
+    const int rows = vertical ? (h + st - 1) / st : h;
+    bp->start[p + 1] = bp->start[p] + bp->tiles[p] * rows;
+  }
+  return dim3(bp->start[planes]);
 }
-inline dim3 BlurHGrid(int w, int h, int planes, const BlurPlanes& bp) {
-  const int st = MinStep(planes, bp);
-  return dim3(((w + st - 1) / st + kBlurTile - 1) / kBlurTile, h, planes);
-}
-inline dim3 BlurVGrid(int w, int h, int planes, const BlurPlanes& bp) {
-  const int st = MinStep(planes, bp);
-  return dim3(((w + st - 1) / st + 255) / 256, (h + st - 1) / st, planes);
-}
+inline dim3 BlurHGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, false); }
+inline dim3 BlurVGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, true); }
 inline RowsPlain Rows(const BlurPlanes& bp, int w) {
   RowsPlain r{};
   for (int p = 0; p < 6; ++p) r.in[p] = bp.in[p];
@@ -418,7 +419,8 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<kBlurRefOpsin><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  const dim3 grid1 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<kBlurRefOpsin><<<grid1, 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_,
                                                                       d_scales_, scale_stride_));
@@ -519,13 +521,15 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigMaskX + c;
   }
-  GZ_TIMED("mask_blur_h", k_blur_h_tiled<kBlurMask><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  const dim3 grid2 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_h", k_blur_h_tiled<kBlurMask><<<grid2, 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  GZ_TIMED("mask_blur_v", k_blur_v<kBlurMask><<<BlurVGrid(w_, h_, 3, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  const dim3 grid3 = BlurVGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_v", k_blur_v<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -553,7 +557,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.out[c] = d_tmp_ + c * n;
     bp.sig[c] = kSigOpsin;
   }
-  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<kBlurOpsin><<<BlurHGrid(w_, h_, 3, bp), 256, 0, s>>>(
+  const dim3 grid4 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<kBlurOpsin><<<grid4, 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_,
                                                                   d_scales_, scale_stride_));
@@ -572,13 +577,15 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.sig[c] = sig;
     bp.sig[3 + c] = sig;
   }
-  GZ_TIMED("edge_blur_h", k_blur_h_tiled<kBlurEdge><<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+  const dim3 grid5 = BlurHGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("edge_blur_h", k_blur_h_tiled<kBlurEdge><<<grid5, 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   for (int p = 0; p < 6; ++p) {
     bp.in[p] = d_tmp_ + p * n;
     bp.out[p] = d_bl_ + p * n;
   }
-  GZ_TIMED("edge_blur_v", k_blur_v<kBlurEdge><<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  const dim3 grid6 = BlurVGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("edge_blur_v", k_blur_v<kBlurEdge><<<grid6, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
@@ -594,7 +601,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.sig[3 + c] = kSigLowFreq;
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<kBlurLowFreq><<<BlurHGrid(w_, h_, 6, bp), 256, 0, s>>>(
+  const dim3 grid7 = BlurHGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<kBlurLowFreq><<<grid7, 256, 0, s>>>(
       Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
@@ -603,7 +611,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    GZ_TIMED("lowfreq_blur_v", k_blur_v<kBlurLowFreq><<<BlurVGrid(w_, h_, 6, bp), 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    const dim3 grid8 = BlurVGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("lowfreq_blur_v", k_blur_v<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -627,11 +636,13 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     BlurPlanes bd{};
     bd.out[0] = d_tmp_;
     bd.sig[0] = kSigDiffmap;
-    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<kBlurDiffmap><<<BlurHGrid(wc, hc, 1, bd), 256, 0, s>>>(
+    const dim3 grid9 = BlurHGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<kBlurDiffmap><<<grid9, 256, 0, s>>>(
         RowsDiffmap{d_resval_, rw_}, bd, wc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    GZ_TIMED("diffmap_blur_v", k_blur_v<kBlurDiffmap><<<BlurVGrid(wc, hc, 1, bd), 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
+    const dim3 grid10 = BlurVGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_v", k_blur_v<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,

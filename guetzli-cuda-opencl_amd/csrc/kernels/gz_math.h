@@ -56,6 +56,11 @@ struct BlurPlanes {
   const float* in[6];
   float* out[6];
   int sig[6];
+  // packed 1-D grid over the planes' (tile, row) work items: plane p owns
+  // workgroups [start[p], start[p+1]), tiles[p] 256-wide tiles per row
+  int nplanes;
+  int tiles[6];
+  int start[7];
 };
 
 // Defined once in gz_device.hip (the single device translation unit).
