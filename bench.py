@@ -179,6 +179,7 @@ def main():
     world, rank, local, dist = dist_setup(args.gpus)
     import torch
     import guetzli_amd as gz
+    from guetzli_amd import sharding
 
     dev = local
     torch.cuda.set_device(dev)
@@ -205,16 +206,9 @@ def main():
         res = list(pool.map(encode, frames[s]))
         out = [r[0] for r in res]
         if dist is not None:
-            # gather the JPEG byte strings to rank 0 over RCCL/xGMI
-            blob = b"".join(out)
-            n = torch.tensor([len(blob)], dtype=torch.int64, device=f"cuda:{dev}")
-            ns = [torch.zeros_like(n) for _ in range(world)]
-            dist.all_gather(ns, n)
-            mx = int(max(x.item() for x in ns))
-            buf = torch.zeros(mx, dtype=torch.uint8, device=f"cuda:{dev}")
-            buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(buf.device)
-            bufs = [torch.zeros_like(buf) for _ in range(world)]
-            dist.all_gather(bufs, buf)
+            # the final gather of the JPEG byte strings over RCCL/xGMI
+            gathered = sharding.gather_bytes(out, dist, "cuda:%d" % dev)
+            assert gathered[rank] == out
         return [len(o) for o in out], [r[1] for r in res]
 
     for s in range(args.warmup):
