@@ -48,11 +48,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def stage_bytes_per_px():
     s = {}
     s["coeffs_to_linear"] = 3 * 2 + 3 * 4          # int16 coeffs -> 3 f32 planes
-    s["opsin_blur_h"] = 3 * 4 + 3 * 4
-    s["opsin_v"] = 3 * 4 + 3 * 4 + 3 * 4           # tmp + linear -> xyb
+    s["opsin"] = 3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 3 * 4  # S1 blur (3->3) + S2 transform (6->3)
     s["mhic"] = 6 * 4 + 6 * 4
-    s["edge_blur_h"] = 6 * 4 + 6 * 4
-    s["edge_blur_v"] = 6 * 4 + 6 * 4
+    s["edge_blur"] = 6 * 4 + 6 * 4                  # S4: 6 separable blurs, 6 -> 6
     s["edge_map"] = 6 * 4 + 3 * 4 / 9.0
     s["block_diff"] = 6 * 4 + 6 * 4 / 9.0
     s["lowfreq_blur_h"] = 6 * 4 + 6 * 4 / 4.0
@@ -73,19 +71,18 @@ def stage_bytes_per_px():
 
 # The "blur+mask pass" of BASELINE.json / SURVEY.md 8(d): blurs S1, S4, S7,
 # S16 and the mask chain S9-S13, 272 algorithmic B/px.  Kernels that carry
-# those stages (opsin_v also does the S2 transform, combine the S13 LUTs with
+# those stages (the opsin kernel also does the S2 transform, combine the S13 LUTs with
 # S14/S15) are timed whole, so the extra fused work only lowers the figure.
 BLUR_MASK_BYTES_PER_PX = 272.0
-BLUR_MASK_STAGES = ("opsin_blur_h", "opsin_v", "edge_blur_h", "edge_blur_v", "lowfreq_blur_h",
+BLUR_MASK_STAGES = ("opsin", "edge_blur", "lowfreq_blur_h",
                     "lowfreq_blur_v", "mask_diff_precompute", "mask_average5x5", "mask_min4_v",
                     "mask_min4_h", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
 STAGE_SYMBOL = {
-    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_blur_h": "void gz::k_blur_h_tiled<1,",
-    "opsin_v": "gz::k_opsin_v(", "mhic": "gz::k_mhic(", "edge_blur_h": "void gz::k_blur_h_tiled<2,",
-    "edge_blur_v": "void gz::k_blur_v<2>(", "edge_map": "gz::k_edge_map(",
+    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin": "gz::k_opsin2d(",
+    "mhic": "gz::k_mhic(", "edge_blur": "void gz::k_blur2d<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h_tiled<3,",
     "lowfreq_blur_v": "void gz::k_blur_v<3>(", "low_freq": "gz::k_low_freq(",
     "mask_diff_precompute": "gz::k_diff_precompute(", "mask_average5x5": "gz::k_average5x5(",

@@ -298,6 +298,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
         if ((kBlurTile - 1) * b.step + 2 * b.radius + 1 + b.step > kBlurLds || 2 * b.radius + 1 > kMaxTaps ||
             b.step < 1 || b.step > 4)
           return fail("blur spec exceeds the tiled kernel's LDS span");
+      for (int sig = kSigEdgeX; sig <= kSigEdgeB; ++sig)
+        if (t.blur[sig].step != 1 || t.blur[sig].radius > kB2MaxR)
+          return fail("edge blur spec does not fit the fused 2-D kernel");
       if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(t)) != hipSuccess)
         return fail("table upload failed");
       g_tab_uploaded[device] = true;
@@ -413,17 +416,11 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
   GZ_HIP(hipSetDevice(device_));
   GZ_HIP(hipMemcpyAsync(d_rgb_, rgb, 3 * n_, device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   GZ_TIMED("ref_linear", k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_rgb_, n_, d_lin_));
-  BlurPlanes bp{};
-  for (int c = 0; c < 3; ++c) {
-    bp.in[c] = d_lin_ + c * n_;
-    bp.out[c] = d_tmp_ + c * n_;
-    bp.sig[c] = kSigOpsin;
+  {
+    const int tx = (w_ + kOpTX - 1) / kOpTX, ty = (h_ + kOpTY - 1) / kOpTY;
+    GZ_TIMED("ref_opsin", k_opsin2d<<<tx * ty, 256, 0, s>>>(d_lin_, w_, h_, tx, d_ref_xyb_, d_scales_,
+                                                              scale_stride_));
   }
-  const dim3 grid1 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("ref_opsin_blur_h", k_blur_h_tiled<kBlurRefOpsin><<<grid1, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
-  GZ_TIMED("ref_opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_ref_xyb_,
-                                                                      d_scales_, scale_stride_));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
   have_mask_scale_ = false;
@@ -550,42 +547,35 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // S0: candidate coefficients -> linear RGB
   GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_));
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
-  // S1/S2: opsin dynamics
-  BlurPlanes bp{};
-  for (int c = 0; c < 3; ++c) {
-    bp.in[c] = d_lin_ + c * n;
-    bp.out[c] = d_tmp_ + c * n;
-    bp.sig[c] = kSigOpsin;
+  // S1/S2: opsin dynamics (blur + transform fused)
+  {
+    const int tx = (w_ + kOpTX - 1) / kOpTX, ty = (h_ + kOpTY - 1) / kOpTY;
+    GZ_TIMED("opsin", k_opsin2d<<<tx * ty, 256, 0, s>>>(d_lin_, w_, h_, tx, d_xyb_, d_scales_,
+                                                          scale_stride_));
   }
-  const dim3 grid4 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("opsin_blur_h", k_blur_h_tiled<kBlurOpsin><<<grid4, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
-  GZ_TIMED("opsin_v", k_opsin_v<<<PixGrid(w_, h_), 256, 0, s>>>(d_tmp_, d_lin_, w_, h_, d_xyb_,
-                                                                  d_scales_, scale_stride_));
   if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   // S3: high intensity change masking
   GZ_TIMED("mhic", k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_));
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
   if (dbg && !d2h(dbg->mhic1, d_m1_, 3 * n)) return false;
-  // S4/S5: edge detector map
-  for (int c = 0; c < 3; ++c) {
-    const int sig = kSigEdgeX + c;
-    bp.in[c] = d_m0_ + c * n;
-    bp.in[3 + c] = d_m1_ + c * n;
-    bp.out[c] = d_tmp_ + c * n;
-    bp.out[3 + c] = d_tmp_ + (3 + c) * n;
-    bp.sig[c] = sig;
-    bp.sig[3 + c] = sig;
+  // S4/S5: edge detector map (6 step-1 blurs of radius <= 3, fused 2-D)
+  {
+    Blur2DPlanes b2{};
+    for (int c = 0; c < 3; ++c) {
+      const int sig = kSigEdgeX + c;
+      b2.in[c] = d_m0_ + c * n;
+      b2.in[3 + c] = d_m1_ + c * n;
+      b2.out[c] = d_bl_ + c * n;
+      b2.out[3 + c] = d_bl_ + (3 + c) * n;
+      b2.sig[c] = sig;
+      b2.sig[3 + c] = sig;
+    }
+    b2.nplanes = 6;
+    b2.tiles_x = (w_ + kB2TX - 1) / kB2TX;
+    b2.tiles_y = (h_ + kB2TY - 1) / kB2TY;
+    GZ_TIMED("edge_blur", k_blur2d<kBlurEdge><<<b2.nplanes * b2.tiles_x * b2.tiles_y, 256, 0, s>>>(
+        b2, w_, h_, d_scales_, scale_stride_));
   }
-  const dim3 grid5 = BlurHGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("edge_blur_h", k_blur_h_tiled<kBlurEdge><<<grid5, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
-  for (int p = 0; p < 6; ++p) {
-    bp.in[p] = d_tmp_ + p * n;
-    bp.out[p] = d_bl_ + p * n;
-  }
-  const dim3 grid6 = BlurVGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("edge_blur_v", k_blur_v<kBlurEdge><<<grid6, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
@@ -594,6 +584,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
   // S7/S8: low-frequency edge term (sigma 14, step 4)
+  BlurPlanes bp{};
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_m0_ + c * n;
     bp.in[3 + c] = d_m1_ + c * n;
