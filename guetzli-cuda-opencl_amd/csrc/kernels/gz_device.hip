@@ -298,6 +298,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
         if ((kBlurTile - 1) * b.step + 2 * b.radius + 1 + b.step > kBlurLds || 2 * b.radius + 1 > kMaxTaps ||
             b.step < 1 || b.step > 4)
           return fail("blur spec exceeds the tiled kernel's LDS span");
+      for (int sig = 0; sig < kNumSigmas; ++sig)
+        if (t.blur[sig].step != kBlurGeomStep[sig] || t.blur[sig].radius != kBlurGeomR[sig])
+          return fail("blur geometry differs from the compiled BlurGeom table");
       for (int sig = kSigEdgeX; sig <= kSigEdgeB; ++sig)
         if (t.blur[sig].step != 1 || t.blur[sig].radius > kB2MaxR)
           return fail("edge blur spec does not fit the fused 2-D kernel");

@@ -30,6 +30,37 @@ enum SigmaId : int {
   kSigDiffmap = 8, // 8.8510880283 (border_ratio 0.03027655136) CalculateDiffmapOpt :958
 };
 
+// Compile-time geometry of the nine blurs (BlurOpt, clbutter_comparator.cpp:
+// 60-69: radius = max(1, int(2.25f * sigma)), step = max(1, int(sigma / 3))),
+// so that tap loops unroll with the taps in scalar registers.  Checked
+// against the host-built table when an engine is created.
+template <int kSig> struct BlurGeom;
+template <> struct BlurGeom<kSigOpsin> { static constexpr int R = 2, STEP = 1; };
+template <> struct BlurGeom<kSigEdgeX> { static constexpr int R = 3, STEP = 1; };
+template <> struct BlurGeom<kSigEdgeY> { static constexpr int R = 1, STEP = 1; };
+template <> struct BlurGeom<kSigEdgeB> { static constexpr int R = 1, STEP = 1; };
+template <> struct BlurGeom<kSigLowFreq> { static constexpr int R = 31, STEP = 4; };
+template <> struct BlurGeom<kSigMaskX> { static constexpr int R = 21, STEP = 3; };
+template <> struct BlurGeom<kSigMaskY> { static constexpr int R = 32, STEP = 4; };
+template <> struct BlurGeom<kSigMaskB> { static constexpr int R = 10, STEP = 1; };
+template <> struct BlurGeom<kSigDiffmap> { static constexpr int R = 19, STEP = 2; };
+constexpr int kBlurGeomR[9] = {2, 3, 1, 1, 31, 21, 32, 10, 19};
+constexpr int kBlurGeomStep[9] = {1, 1, 1, 1, 4, 3, 4, 1, 2};
+
+// Calls F(kSig) for the (uniform) runtime sigma id.
+#define GZ_BLUR_SWITCH(sig, F)            \
+  switch (sig) {                          \
+    case kSigOpsin: F(kSigOpsin); break;  \
+    case kSigEdgeX: F(kSigEdgeX); break;  \
+    case kSigEdgeY: F(kSigEdgeY); break;  \
+    case kSigEdgeB: F(kSigEdgeB); break;  \
+    case kSigLowFreq: F(kSigLowFreq); break; \
+    case kSigMaskX: F(kSigMaskX); break;  \
+    case kSigMaskY: F(kSigMaskY); break;  \
+    case kSigMaskB: F(kSigMaskB); break;  \
+    default: F(kSigDiffmap); break;       \
+  }
+
 struct BlurSpec {
   int radius;          // "diff" in BlurOpt
   int step;            // xstep == ystep
