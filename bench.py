@@ -113,6 +113,20 @@ def measured_traffic(stage, w, h):
     return None, None
 
 
+def _thread_cpu():
+    """{tid: (cpu seconds, name)} of this process's threads."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            st = open("/proc/self/task/%s/stat" % tid).read()
+            f = st[st.rindex(")") + 2:].split()
+            out[tid] = ((int(f[11]) + int(f[12])) / tick, st[st.index("(") + 1:st.rindex(")")])
+        except (OSError, ValueError):
+            pass
+    return out
+
+
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -213,6 +227,9 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    import resource
+    t_before = _thread_cpu() if os.environ.get("GZ_THREAD_CPU") else {}
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     iters = []
     conc = {}
@@ -228,6 +245,15 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    if os.environ.get("GZ_THREAD_CPU"):
+        # per-thread CPU seconds spent inside the timed region (diagnostic)
+        t_after = _thread_cpu()
+        rows = sorted(((c - t_before.get(k, (0.0, ""))[0], n) for k, (c, n) in t_after.items()),
+                      reverse=True)
+        print("thread cpu:", [(round(c, 3), n) for c, n in rows[:24] if c > 0.001], file=sys.stderr)
+    cpu_per_frame = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / (
+        args.steps * args.frames_per_step)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -325,6 +351,7 @@ def main():
         "block_zeroing": {"launches": bz[0], "avg_ms": round(bz[1] / bz[0], 3)} if bz else None,
         "stages": stages,
         "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
+        "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
         "single_frame": {"seconds": round(single_s, 4),
                          "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
                          "iterations": st1.iterations,

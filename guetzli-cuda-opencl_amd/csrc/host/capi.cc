@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "host/jpeg_encode.h"
+#include "host/jpeg_writer.h"
 #include "host/processor.h"
 #include "host/synthetic.h"
 #include "runtime/engine.h"
@@ -164,6 +165,54 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
                             reinterpret_cast<gz::CoeffDataHost*>(out)))
     return SetError(GZ_ERR_DEVICE, "block_zeroing_orders: " + e.error());
   return GZ_OK;
+}
+
+static gz_status CopyOut(const std::string& s, uint8_t** jpeg_out, size_t* jpeg_size) {
+  uint8_t* buf = static_cast<uint8_t*>(std::malloc(s.size() ? s.size() : 1));
+  if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "out of host memory");
+  std::memcpy(buf, s.data(), s.size());
+  *jpeg_out = buf;
+  *jpeg_size = s.size();
+  return GZ_OK;
+}
+
+gz_status gz_comparator_write_jpeg(gz_comparator* cmp, const int16_t* coeffs, const int* quant,
+                                   uint8_t** jpeg_out, size_t* jpeg_size) {
+  if (!cmp || !coeffs || !quant || !jpeg_out || !jpeg_size)
+    return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: bad argument");
+  int q[3][64];
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) {
+      q[c][k] = quant[c * 64 + k];
+      if (q[c][k] < 1 || q[c][k] > 65535) return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: quant");
+    }
+  gz::Engine& e = *cmp->engine;
+  if (!e.UploadCoeffs(coeffs)) return SetError(GZ_ERR_DEVICE, "write_jpeg: " + e.error());
+  gz::JpegData meta;
+  std::string out, err;
+  if (!gz::DeviceWriteJpeg(&e, cmp->w, cmp->h, q, meta, true, &out, &err))
+    return SetError(GZ_ERR_DEVICE, "write_jpeg: " + err);
+  return CopyOut(out, jpeg_out, jpeg_size);
+}
+
+gz_status gz_write_jpeg_host(int width, int height, const int16_t* coeffs, const int* quant,
+                             uint8_t** jpeg_out, size_t* jpeg_size) {
+  if (!coeffs || !quant || !jpeg_out || !jpeg_size || width <= 0 || height <= 0)
+    return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: bad argument");
+  gz::CoeffImage img;
+  img.Init(width, height);
+  std::memcpy(img.coeffs.data(), coeffs, img.coeffs.size() * sizeof(int16_t));
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) {
+      img.quant[c][k] = quant[c * 64 + k];
+      if (img.quant[c][k] < 1 || img.quant[c][k] > 65535)
+        return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: quant");
+    }
+  gz::JpegData jpg;
+  img.SaveToJpegData(&jpg);
+  std::string out;
+  if (!gz::WriteJpegReference(jpg, true, &out)) return SetError(GZ_ERR_INTERNAL, "write_jpeg_host");
+  return CopyOut(out, jpeg_out, jpeg_size);
 }
 
 size_t gz_last_process_detail(char* buf, size_t cap) {

@@ -108,24 +108,28 @@ bool CoeffImage::ComponentIsAllZero(int c) const {
   return true;
 }
 
-void CoeffImage::SaveHeaderToJpegData(int ncomp, JpegData* jpg) const {
-  jpg->width = width;
-  jpg->height = height;
+void JpegHeaderFor(int w, int h, const int q[3][kDCTBlockSize], int ncomp, JpegData* jpg) {
+  jpg->width = w;
+  jpg->height = h;
   jpg->max_h_samp_factor = 1;
   jpg->max_v_samp_factor = 1;
-  jpg->mcu_cols = block_w;
-  jpg->mcu_rows = block_h;
+  jpg->mcu_cols = (w + 7) / 8;
+  jpg->mcu_rows = (h + 7) / 8;
   jpg->components.resize(ncomp);
   for (int c = 0; c < ncomp; ++c) {
     JpegComponent& comp = jpg->components[c];
     comp.id = c;
     comp.h_samp_factor = 1;
     comp.v_samp_factor = 1;
-    comp.width_in_blocks = block_w;
-    comp.height_in_blocks = block_h;
+    comp.width_in_blocks = jpg->mcu_cols;
+    comp.height_in_blocks = jpg->mcu_rows;
     comp.coeffs.clear();
   }
-  SaveQuantTables(quant, jpg);
+  SaveQuantTables(q, jpg);
+}
+
+void CoeffImage::SaveHeaderToJpegData(int ncomp, JpegData* jpg) const {
+  JpegHeaderFor(width, height, quant, ncomp, jpg);
 }
 
 void CoeffImage::SaveToJpegData(JpegData* jpg) const {

@@ -65,12 +65,16 @@ struct CoeffImage {
   // `changed`.  A mirror remembers the (epoch, journal length) it reflects.
   uint64_t epoch = 0;
   std::vector<uint32_t> changed;
+  // False while only a device mirror holds the current coefficients (after a
+  // device-side global quantization whose host copy was not requested).
+  bool host_valid = true;
   void MarkChanged(int c, int block_ix, int k) {
     changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * blocks + block_ix) * 64 + k));
   }
-  void BulkChanged() {
+  void BulkChanged() {  // (also: the host copy is the authoritative one)
     ++epoch;
     changed.clear();
+    host_valid = true;
   }
 
   void Init(int w, int h);
@@ -101,6 +105,10 @@ struct CoeffCursor {
     pos = img.changed.size();
   }
 };
+
+// The header part of SaveToJpegData for a w x h 4:4:4 image with quant q and
+// ncomp stored components (components without coefficients).
+void JpegHeaderFor(int w, int h, const int q[3][kDCTBlockSize], int ncomp, JpegData* jpg);
 
 // Quantize (guetzli/quantize.h:25-30)
 inline coeff_t QuantizeCoeff(coeff_t raw, int quant) {

@@ -81,10 +81,7 @@ class BitSink {
   int free_ = 64;
 };
 
-struct HuffTable {
-  uint8_t depth[256];
-  int code[256];
-};
+using HuffTable = HuffCodeTable;
 
 void BuildCodeCounts(const uint8_t* depth, int* counts, int* values) {
   // BuildHuffmanCode, jpeg_data_writer.cc:138-153
@@ -910,6 +907,40 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
 
 bool WriteJpegReference(const JpegData& jpg, bool strip_metadata, std::string* out) {
   return WriteJpegSerial(jpg, strip_metadata, out);
+}
+
+bool WriteJpegPrologue(const JpegData& hdr, bool strip_metadata, JpegHistogram* dc_h,
+                       JpegHistogram* ac_h, HuffCodeTable* dc_tab, HuffCodeTable* ac_tab,
+                       std::string* out) {
+  if (!WriteHeaderSegments(hdr, strip_metadata, out)) return false;
+  WriteHuffmanSegments(hdr, dc_h, ac_h, dc_tab, ac_tab, out);
+  return true;
+}
+
+void AppendStuffedScan(const uint8_t* bits_be, uint64_t nbits, std::string* out) {
+  // pad the last byte with one bits, 0xff -> 0xff 0x00 (BitWriter::
+  // JumpToByteBoundary / EmitByte, jpeg_bit_writer.h), then EOI
+  const uint64_t full = nbits / 8;
+  const int rem = static_cast<int>(nbits % 8);
+  out->reserve(out->size() + full + full / 128 + 8);
+  const uint8_t* p = bits_be;
+  const uint8_t* end = bits_be + full;
+  while (p < end) {
+    const uint8_t* ff = static_cast<const uint8_t*>(std::memchr(p, 0xff, end - p));
+    if (!ff) {
+      out->append(reinterpret_cast<const char*>(p), end - p);
+      break;
+    }
+    out->append(reinterpret_cast<const char*>(p), ff + 1 - p);
+    out->push_back(0);
+    p = ff + 1;
+  }
+  if (rem) {
+    const uint8_t b = static_cast<uint8_t>(bits_be[full] | (0xff >> rem));
+    out->push_back(static_cast<char>(b));
+    if (b == 0xff) out->push_back(0);
+  }
+  out->append("\xff\xd9", 2);
 }
 
 }  // namespace gz

@@ -26,6 +26,12 @@ struct JpegHistogram {
   int NumSymbols() const;
 };
 
+// A component's Huffman code: bit length and code of each symbol.
+struct HuffCodeTable {
+  uint8_t depth[256];
+  int code[256];
+};
+
 // Length-limited Huffman code lengths (CreateHuffmanTree, entropy_encode.cc:65-145).
 void HuffmanCodeLengths(const uint32_t* counts, int length, int max_depth, uint8_t* depth);
 
@@ -41,6 +47,16 @@ size_t ClusterHistograms(JpegHistogram* histo, size_t* num, int* histo_indexes, 
 bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out);
 // The serial writer, always (test comparison baseline).
 bool WriteJpegReference(const JpegData& jpg, bool strip_metadata, std::string* out);
+
+// Everything before the entropy-coded scan for the component histograms
+// dc_h / ac_h (clobbered): SOI, metadata, DQT, SOF1, DHT, SOS; fills the
+// per-component code tables the scan is encoded with.
+bool WriteJpegPrologue(const JpegData& hdr, bool strip_metadata, JpegHistogram* dc_h,
+                       JpegHistogram* ac_h, HuffCodeTable* dc_tab, HuffCodeTable* ac_tab,
+                       std::string* out);
+// Appends an unstuffed scan bitstream (MSB-first bytes, nbits bits): pads
+// the last byte with ones, byte-stuffs 0xff, appends EOI.
+void AppendStuffedScan(const uint8_t* bits_be, uint64_t nbits, std::string* out);
 
 // Reusable scratch of the staged encoder.
 struct ScanScratch;

@@ -126,6 +126,10 @@ bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
 // journalled edits when it is in img's epoch, else everything.
 bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
   if (device_.Current(img)) return true;
+  if (!img.host_valid) {
+    err_ = "coefficients are current on neither side";
+    return false;
+  }
   bool ok;
   if (device_.CanReplay(img) && img.changed.size() - device_.pos < img.coeffs.size() / 8) {
     const size_t n = img.changed.size() - device_.pos;
@@ -156,27 +160,87 @@ bool HipButteraugliComparator::Compare(const CoeffImage& img) {
   return true;
 }
 
-bool HipButteraugliComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) {
+bool HipButteraugliComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
+                                                    bool need_host) {
   // CopyFromJpegData(q=1) + ApplyGlobalQuantization (processor.cc:316-317)
-  // on both sides: the device quantizes its copy of the originals, the host
-  // its own (the same integer function; no 2-byte-per-coefficient download).
-  if (!engine_->QuantizeFromOriginal(q, nullptr)) {
+  // on the device copy of the originals; the host copy (a pinned DMA) only
+  // when the caller will read it.
+  if (!engine_->QuantizeFromOriginal(q, need_host ? img->coeffs.data() : nullptr)) {
     err_ = engine_->error();
     return false;
   }
-  const size_t per = static_cast<size_t>(img->blocks) * 64;
-  const size_t chunk = 1 << 16;
-  const int nchunks = static_cast<int>((3 * per + chunk - 1) / chunk);
-  coeff_t* dst = img->coeffs.data();
-  const coeff_t* src = orig_.data();
-  ParallelFor(nchunks, [&](int ch) {
-    const size_t b = ch * chunk, e = std::min(3 * per, b + chunk);
-    for (size_t i = b; i < e; ++i) dst[i] = QuantizeCoeff(src[i], q[i / per][i & 63]);
-  });
   for (int c = 0; c < 3; ++c) std::memcpy(img->quant[c], q[c], sizeof(img->quant[c]));
   img->BulkChanged();
+  img->host_valid = need_host;
   device_.Set(*img);
   return true;
+}
+
+int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram dc[3],
+                         JpegHistogram ac[3], std::string* err) {
+  uint32_t hist[6 * 256];
+  uint64_t chroma = 0;
+  if (!e->JpegStage(q, hist, &chroma)) {
+    if (err) *err = e->error();
+    return -1;
+  }
+  const int ncomp = chroma > 0 ? 3 : 1;  // SaveToJpegData drops all-zero chroma
+  for (int c = 0; c < 3; ++c) {
+    dc[c].Clear();
+    ac[c].Clear();
+    if (c >= ncomp) continue;
+    for (int i = 0; i < 256; ++i) {
+      dc[c].counts[i] = 2 * hist[(2 * c) * 256 + i];
+      ac[c].counts[i] = 2 * hist[(2 * c + 1) * 256 + i];
+    }
+  }
+  return ncomp;
+}
+
+bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                     bool strip_metadata, std::string* out, std::string* err) {
+  JpegHistogram dc_h[3], ac_h[3];
+  const int ncomp = DeviceJpegHistograms(e, q, dc_h, ac_h, err);
+  if (ncomp < 0) return false;
+  JpegData hdr;
+  hdr.app_data = meta.app_data;
+  hdr.com_data = meta.com_data;
+  JpegHeaderFor(w, h, q, ncomp, &hdr);
+  HuffCodeTable dc_tab[3], ac_tab[3];
+  out->clear();
+  if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, out)) {
+    if (err) *err = "jpeg header";
+    return false;
+  }
+  JpegCodeTables codes;
+  std::memset(&codes, 0, sizeof(codes));
+  for (int c = 0; c < ncomp; ++c)
+    for (int i = 0; i < 256; ++i) {
+      codes.dc_len[c][i] = dc_tab[c].depth[i];
+      codes.ac_len[c][i] = ac_tab[c].depth[i];
+      codes.dc_code[c][i] = static_cast<uint16_t>(dc_tab[c].code[i]);
+      codes.ac_code[c][i] = static_cast<uint16_t>(ac_tab[c].code[i]);
+    }
+  const uint8_t* bytes = nullptr;
+  uint64_t nbits = 0;
+  if (!e->JpegScan(ncomp, codes, &bytes, &nbits)) {
+    if (err) *err = e->error();
+    return false;
+  }
+  AppendStuffedScan(bytes, nbits, out);
+  return true;
+}
+
+int HipButteraugliComparator::DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3],
+                                               JpegHistogram ac[3]) {
+  if (!SyncCoeffs(img)) return -1;
+  return DeviceJpegHistograms(engine_.get(), img.quant, dc, ac, &err_);
+}
+
+bool HipButteraugliComparator::DeviceWriteJpeg(const CoeffImage& img, const JpegData& meta,
+                                               bool strip_metadata, std::string* out) {
+  if (!SyncCoeffs(img)) return false;
+  return gz::DeviceWriteJpeg(engine_.get(), w_, h_, img.quant, meta, strip_metadata, out, &err_);
 }
 
 bool HipButteraugliComparator::StartBlockComparisons() {
@@ -535,11 +599,21 @@ class Processor {
   // MaybeOutput of a candidate must see the distance of the Compare that
   // followed it, so it is applied by FlushOutput, which runs before the next
   // Compare (at the next BeginOutput) or explicitly.
-  void BeginOutput(const JpegData& jpg, const CoeffImage& img) {
+  bool BeginOutput(const JpegData& jpg, const CoeffImage& img, std::string* err) {
     FlushOutput();
     const auto t0 = Clock::now();
-    StageCoeffImage(img, jpg, scratch_.get());
     pending_.clear();
+    if (cmp_->HasDeviceWriter()) {
+      // entropy coded on the device from its resident copy (sub-ms), no
+      // helper thread needed
+      if (!cmp_->DeviceWriteJpeg(img, jpg, params_.clear_metadata, &pending_)) return Fail(err);
+      has_pending_ = true;
+      const double dt = Since(t0);
+      res_->seconds_write += dt;
+      res_->detail["write_device_s"] += dt;
+      return true;
+    }
+    StageCoeffImage(img, jpg, scratch_.get());
     writer_ = std::thread([this] {
       const auto t = Clock::now();
       EncodeStaged(scratch_.get(), params_.clear_metadata, &pending_);
@@ -549,16 +623,19 @@ class Processor {
     const double dt = Since(t0);
     res_->seconds_write += dt;
     res_->detail["write_stage_s"] += dt;
+    return true;
   }
   // Joins the pending encode and applies its MaybeOutput; returns its size.
   size_t FlushOutput() {
     if (!has_pending_) return 0;
-    const auto t0 = Clock::now();
-    writer_.join();
-    const double dt = Since(t0);
-    res_->seconds_write += dt;
-    res_->detail["write_wait_s"] += dt;
-    res_->detail["write_encode_s"] += encode_s_;
+    if (writer_.joinable()) {
+      const auto t0 = Clock::now();
+      writer_.join();
+      const double dt = Since(t0);
+      res_->seconds_write += dt;
+      res_->detail["write_wait_s"] += dt;
+      res_->detail["write_encode_s"] += encode_s_;
+    }
     has_pending_ = false;
     MaybeOutput(pending_);
     return pending_.size();
@@ -598,9 +675,9 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
   // processor.cc:310-338
   std::memcpy(data->q, q, sizeof(data->q));
   const auto tq = Clock::now();
-  if (!cmp_->QuantizeFromOriginal(q, img)) return Fail(err);
+  if (!cmp_->QuantizeFromOriginal(q, img, /*need_host=*/!cmp_->HasDeviceWriter())) return Fail(err);
   res_->seconds_quantize += Since(tq);
-  BeginOutput(jpg_in, *img);
+  if (!BeginOutput(jpg_in, *img, err)) return false;
   ++res_->iterations;
   if (!cmp_->Compare(*img)) return Fail(err);
   data->dist_ok = cmp_->DistanceOK(target_mul);
@@ -662,7 +739,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   int jpg_header_size, dc_size;
   {
     JpegHistogram dc_h[3], ac_h[3];
-    const int saved = CoeffImageHistograms(*img, scratch_.get(), dc_h, ac_h);
+    int saved = cmp_->DeviceHistograms(*img, dc_h, ac_h);
+    if (saved < 0 && cmp_->HasDeviceWriter()) return Fail(err);
+    if (saved < 0) saved = CoeffImageHistograms(*img, scratch_.get(), dc_h, ac_h);
     JpegData out;
     out.app_data = jpg.app_data;
     out.com_data = jpg.com_data;
@@ -798,7 +877,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
-      BeginOutput(jpg, *img);
+      if (!BeginOutput(jpg, *img, err)) return false;
       if (!cmp_->Compare(*img)) return Fail(err);
       prev_size = est_jpg_size;
     }

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "host/jpeg_model.h"
+#include "host/jpeg_writer.h"
 #include "runtime/engine.h"
 
 namespace gz {
@@ -46,7 +47,22 @@ class Comparator {
                                       std::vector<uint8_t>* idx, std::vector<float>* err);
   // CopyFromJpegData(q=1) + ApplyGlobalQuantization(q) of the originals into img
   // (and into any device mirror).
-  virtual bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) = 0;
+  // need_host false: only the comparator's own (device) copy must be
+  // current; img->coeffs may be left stale (img->host_valid = false).
+  virtual bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
+                                    bool need_host = true) = 0;
+  // Entropy coding of img (SaveToJpegData over meta + WriteJpeg) by the
+  // comparator's device; HasDeviceWriter() false: use the host writer.
+  virtual bool HasDeviceWriter() const { return false; }
+  virtual bool DeviceWriteJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                               std::string* out) {
+    return false;
+  }
+  // DC / AC histograms of img as SaveToJpegData stores it (comps at or above
+  // the returned count cleared) from the device copy; -1 if unsupported.
+  virtual int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) {
+    return -1;
+  }
   virtual double ScoreOutputSize(int size) const = 0;
   virtual bool DistanceOK(double target_mul) const = 0;
   virtual float distmap_aggregate() const = 0;
@@ -69,6 +85,14 @@ void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int 
                                  const std::vector<float>& max_dist_per_block,
                                  std::vector<float>* block_weight);
 
+// SaveToJpegData + WriteJpeg of the engine's current coefficients (quant q,
+// image w x h, metadata of meta) entropy coded on the device.
+bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                     bool strip_metadata, std::string* out, std::string* err);
+// The histogram stage of it alone (for the search back end's size model).
+int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram dc[3],
+                         JpegHistogram ac[3], std::string* err);
+
 // guetzli::ButteraugliComparator on the HIP engine.
 class HipButteraugliComparator : public Comparator {
  public:
@@ -84,7 +108,12 @@ class HipButteraugliComparator : public Comparator {
   bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
                               int lookahead, std::vector<int>* offsets, std::vector<uint8_t>* idx,
                               std::vector<float>* err) override;
-  bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img) override;
+  bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
+                            bool need_host = true) override;
+  bool HasDeviceWriter() const override { return true; }
+  bool DeviceWriteJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                       std::string* out) override;
+  int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) override;
   double ScoreOutputSize(int size) const override;
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }
   float distmap_aggregate() const override { return distance_; }

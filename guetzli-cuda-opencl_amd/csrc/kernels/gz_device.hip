@@ -27,6 +27,7 @@ __constant__ GzTables c_tab;
 #include "butteraugli_kernels.inc"
 #include "block_zeroing.inc"
 #include "coeff_kernels.inc"
+#include "jpeg_kernels.inc"
 
 namespace gz {
 
@@ -355,6 +356,19 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_coeffs_), nc * sizeof(int16_t)) != hipSuccess)
     ok = false;
+  alloc(reinterpret_cast<void**>(&e->d_jzz_), nc * sizeof(int16_t));
+  alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
+  alloc(reinterpret_cast<void**>(&e->d_jhist_), 6 * 256 * 4 + 16);
+  alloc(&e->d_jcodes_, sizeof(JpegCodeTables));
+  alloc(reinterpret_cast<void**>(&e->d_jbitlen_), static_cast<size_t>(e->nb_) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_jbitoff_), static_cast<size_t>(e->nb_ + 1) * 4);
+  // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
+  e->jwords_cap_ = static_cast<size_t>(e->nb_) * 160 + 16;
+  alloc(reinterpret_cast<void**>(&e->d_jwords_), e->jwords_cap_ * 4);
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 16) != hipSuccess)
+    ok = false;
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodeTables)) != hipSuccess)
+    ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
@@ -400,7 +414,8 @@ Engine::~Engine() {
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
-                  d_delta_val_, d_zero_count_, d_zero_off_, d_cand_idx_, d_cand_err_};
+                  d_delta_val_, d_zero_count_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
+                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
@@ -408,6 +423,9 @@ Engine::~Engine() {
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
   if (h_zero_off_) hipHostFree(h_zero_off_);
   if (h_coeffs_) hipHostFree(h_coeffs_);
+  if (h_jhist_) hipHostFree(h_jhist_);
+  if (h_jcodes_) hipHostFree(h_jcodes_);
+  if (h_jbytes_) hipHostFree(h_jbytes_);
   if (h_cand_idx_) hipHostFree(h_cand_idx_);
   if (h_cand_err_) hipHostFree(h_cand_err_);
   if (h_delta_val_) hipHostFree(h_delta_val_);
@@ -501,11 +519,12 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   memcpy(qm.q, q, sizeof(qm.q));
   const size_t per = static_cast<size_t>(nb_) * 64;
   GZ_TIMED("quantize", k_quantize<<<dim3((per + 255) / 256, 3), 256, 0, s>>>(d_orig_, qm, per, d_cur_));
-  if (host_out) {
-    GZ_HIP(hipMemcpyAsync(host_out, d_cur_, 3 * per * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+  if (host_out) {  // through the pinned staging: a DMA, no pageable bounce
+    GZ_HIP(hipMemcpyAsync(h_coeffs_, d_cur_, 3 * per * sizeof(int16_t), hipMemcpyDeviceToHost, s));
     GZ_HIP(hipStreamSynchronize(s));
-  ProfFlush();
+    memcpy(host_out, h_coeffs_, 3 * per * sizeof(int16_t));
   }
+  ProfFlush();
   return true;
 }
 
@@ -746,6 +765,62 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
   offsets->assign(h_zero_off_, h_zero_off_ + nb_ + 1);
   idx->assign(h_cand_idx_, h_cand_idx_ + total);
   err->assign(h_cand_err_, h_cand_err_ + total);
+  return true;
+}
+
+bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  JpegQuantF qf;
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
+  GZ_HIP(hipMemsetAsync(d_jhist_, 0, 6 * 256 * 4 + 16, s));
+  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * nb_ + 255) / 256, 256, 0, s>>>(
+      d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_,
+      reinterpret_cast<unsigned long long*>(d_jhist_ + 6 * 256)));
+  GZ_HIP(hipMemcpyAsync(h_jhist_, d_jhist_, 6 * 256 * 4 + 8, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  memcpy(hist, h_jhist_, 6 * 256 * 4);
+  uint64_t nz;
+  memcpy(&nz, h_jhist_ + 6 * 256, 8);
+  *chroma_nz = nz;
+  return true;
+}
+
+bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, const uint8_t** bytes, uint64_t* nbits) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
+  // the pinned code staging may still feed the previous scan's copy
+  GZ_HIP(hipStreamSynchronize(s));
+  *h_jcodes_ = codes;
+  GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodeTables), hipMemcpyHostToDevice, s));
+  const JpegCodeTables* dc = static_cast<const JpegCodeTables*>(d_jcodes_);
+  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<(nb_ + 255) / 256, 256, 0, s>>>(d_jzz_, d_jmask_, nb_, ncomp, dc,
+                                                                    d_jbitlen_));
+  GZ_TIMED("jpeg_scan", k_scan_counts<<<1, 1024, 0, s>>>(d_jbitlen_, nb_, d_jbitoff_));
+  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jbitoff_ + nb_, 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  const uint64_t total = h_jhist_[6 * 256 + 2];
+  const size_t words = static_cast<size_t>((total + 31) / 32);
+  if (words + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
+  GZ_HIP(hipMemsetAsync(d_jwords_, 0, (words + 1) * 4, s));
+  GZ_TIMED("jpeg_emit", k_jpeg_emit<<<(nb_ + 255) / 256, 256, 0, s>>>(d_jzz_, d_jmask_, nb_, ncomp, dc,
+                                                                    d_jbitoff_, d_jwords_));
+  if (words * 4 > h_jbytes_cap_) {
+    if (h_jbytes_) GZ_HIP(hipHostFree(h_jbytes_));
+    h_jbytes_ = nullptr;
+    h_jbytes_cap_ = 0;
+    const size_t cap = words * 4 + words + 4096;
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_jbytes_), cap));
+    h_jbytes_cap_ = cap;
+  }
+  if (words) GZ_HIP(hipMemcpyAsync(h_jbytes_, d_jwords_, words * 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  *bytes = h_jbytes_;
+  *nbits = total;
   return true;
 }
 

@@ -23,6 +23,15 @@ struct CoeffDataHost {  // guetzli::CoeffData (processor.h:29-32)
 };
 
 // Optional host destinations for stage-level parity tests.
+// Per component Huffman code (length, code) of every symbol, as the device
+// entropy coder consumes them.
+struct JpegCodeTables {
+  uint8_t dc_len[3][256];
+  uint8_t ac_len[3][256];
+  uint16_t dc_code[3][256];
+  uint16_t ac_code[3][256];
+};
+
 struct CompareDebug {
   float* cand_linear = nullptr;   // 3*w*h
   float* cand_xyb = nullptr;      // 3*w*h
@@ -80,6 +89,15 @@ class Engine {
   bool BlockZeroingCandidates(int comp_mask, float limit, int lookahead, std::vector<int>* offsets,
                               std::vector<uint8_t>* idx, std::vector<float>* err);
 
+  // Device entropy coding of the current coefficients with quant q (the
+  // per-iteration JPEG of the search).  JpegStage: quantized zigzag
+  // coefficients, symbol histograms hist[comp*2 + {0:DC, 1:AC}][256] (plain
+  // counts) and the number of non-zero chroma coefficients.  JpegScan: the
+  // scan bitstream of the staged image for `ncomp` components with `codes`;
+  // *bytes (MSB-first, valid until the next call) holds *nbits bits.
+  bool JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz);
+  bool JpegScan(int ncomp, const JpegCodeTables& codes, const uint8_t** bytes, uint64_t* nbits);
+
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
   double last_kernel_ms(const char* which) const;
@@ -134,6 +152,18 @@ class Engine {
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
   int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
+  int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
+  uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
+  uint32_t* d_jhist_ = nullptr;    //   6 x 256 counts + chroma non-zeros (u64)
+  void* d_jcodes_ = nullptr;       //   JpegCodeTables
+  int* d_jbitlen_ = nullptr;       //   [blocks]
+  int* d_jbitoff_ = nullptr;       //   [blocks + 1]
+  uint32_t* d_jwords_ = nullptr;   //   scan bitstream
+  size_t jwords_cap_ = 0;
+  uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + total bits
+  JpegCodeTables* h_jcodes_ = nullptr;
+  uint8_t* h_jbytes_ = nullptr;
+  size_t h_jbytes_cap_ = 0;
   int* h_zero_off_ = nullptr;      // pinned
   uint8_t* h_cand_idx_ = nullptr;  // pinned, h_cand_cap_ entries
   float* h_cand_err_ = nullptr;

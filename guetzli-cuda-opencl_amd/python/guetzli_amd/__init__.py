@@ -71,7 +71,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
-    "gz_comparator_original_coeffs",
+    "gz_comparator_original_coeffs", "gz_comparator_write_jpeg", "gz_write_jpeg_host",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail",
 )
@@ -120,6 +120,12 @@ def lib():
     L.gz_comparator_block_zeroing_orders.restype = i32
     L.gz_comparator_original_coeffs.argtypes = [vp, vp]
     L.gz_comparator_original_coeffs.restype = i32
+    L.gz_comparator_write_jpeg.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_size_t)]
+    L.gz_comparator_write_jpeg.restype = i32
+    L.gz_write_jpeg_host.argtypes = [i32, i32, vp, vp, ctypes.POINTER(ctypes.c_void_p),
+                                     ctypes.POINTER(ctypes.c_size_t)]
+    L.gz_write_jpeg_host.restype = i32
     L.gz_synthetic_frame.argtypes = [u64, i32, i32, vp]
     L.gz_synthetic_frame.restype = i32
     L.gz_rgb_to_coeffs.argtypes = [vp, i32, i32, vp]
@@ -176,6 +182,24 @@ def last_process_detail():
     buf = ctypes.create_string_buffer(n)
     L.gz_last_process_detail(buf, n)
     return json.loads(buf.value.decode())
+
+
+def _take_bytes(p, n):
+    try:
+        return ctypes.string_at(p.value, n.value)
+    finally:
+        lib().gz_free(p)
+
+
+def write_jpeg_host(coeffs, quant, width, height):
+    """SaveToJpegData + WriteJpeg on the host of dequantized [3][blocks][64]
+    int16 coefficients with [3][64] quant tables (metadata stripped)."""
+    c = np.ascontiguousarray(coeffs, dtype=np.int16).reshape(-1)
+    q = np.ascontiguousarray(quant, dtype=np.int32).reshape(-1)
+    p, n = ctypes.c_void_p(), ctypes.c_size_t()
+    _check(lib().gz_write_jpeg_host(width, height, _ptr(c), _ptr(q), ctypes.byref(p),
+                                    ctypes.byref(n)), "write_jpeg_host")
+    return _take_bytes(p, n)
 
 
 def device_count():
@@ -363,6 +387,15 @@ class ButteraugliComparator:
         _check(lib().gz_comparator_start_block_comparisons(self._h, _ptr(out)),
                "start_block_comparisons")
         return out.reshape(self.blocks, 3)
+
+    def write_jpeg(self, coeffs, quant):
+        """The same JPEG as write_jpeg_host, entropy coded on the device."""
+        c = self._coeffs(coeffs)
+        q = np.ascontiguousarray(quant, dtype=np.int32).reshape(-1)
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().gz_comparator_write_jpeg(self._h, _ptr(c), _ptr(q), ctypes.byref(p),
+                                              ctypes.byref(n)), "write_jpeg")
+        return _take_bytes(p, n)
 
     def original_coeffs(self):
         """q=1 coefficients of the reference image, computed on the device."""

@@ -149,6 +149,17 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
                                              const int16_t* orig_coeffs, int comp_mask,
                                              float limit, int lookahead, gz_coeff_data* out);
 
+/* SaveToJpegData + WriteJpeg (guetzli/output_image.cc:579-640,
+ * jpeg_data_writer.cc:540-553) of dequantized coefficients `coeffs`
+ * ([3][blocks][64], multiples of quant) with quant tables `quant` ([3][64],
+ * natural order), entropy coded on the comparator's device; metadata
+ * stripped.  *jpeg_out is allocated by the library (gz_free). */
+gz_status gz_comparator_write_jpeg(gz_comparator* cmp, const int16_t* coeffs, const int* quant,
+                                   uint8_t** jpeg_out, size_t* jpeg_size);
+/* The same on the host (the library's serial writer; no device needed). */
+gz_status gz_write_jpeg_host(int width, int height, const int16_t* coeffs, const int* quant,
+                             uint8_t** jpeg_out, size_t* jpeg_size);
+
 /* ---- measurement ------------------------------------------------------ */
 /* Per-launch timing with HIP events on each object's own stream (off by
  * default).  Regions are named after the pass stage ("block_diff",

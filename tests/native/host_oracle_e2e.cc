@@ -57,7 +57,7 @@ class OracleComparator : public gz::Comparator {
                              target_, lookahead, reinterpret_cast<gzo_coeff_data*>(out->data()));
     return true;
   }
-  bool QuantizeFromOriginal(const int q[3][64], gz::CoeffImage* img) override {
+  bool QuantizeFromOriginal(const int q[3][64], gz::CoeffImage* img, bool) override {
     const size_t per = static_cast<size_t>(img->blocks) * 64;
     for (int c = 0; c < 3; ++c)
       for (size_t i = 0; i < per; ++i)

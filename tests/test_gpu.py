@@ -103,6 +103,32 @@ def test_device_fdct_matches_host_encoder(gz, w, h, seed):
     assert np.array_equal(cmp.original_coeffs(), gz.rgb_to_coeffs(rgb, w, h))
 
 
+def _quantized(gz, rgb, w, h, quant):
+    c = gz.rgb_to_coeffs(rgb, w, h).reshape(3, -1, 64).astype(np.int32)
+    qq = quant[:, None, :]
+    r = np.fmod(c, qq)
+    return (c + np.where(2 * r > qq, qq - r, np.where(-2 * r > qq, -qq - r, -r))).astype(np.int16)
+
+
+@pytest.mark.parametrize("w,h,seed", [(333, 197, 2), (1920, 1080, 0), (64, 8, 5), (97, 41, 9)])
+def test_device_jpeg_writer_matches_host_writer(gz, w, h, seed):
+    """Device entropy coding (k_jpeg_stage/bits/emit + host tables) ==
+    SaveToJpegData + WriteJpeg on the host, byte for byte: random quant
+    tables (incl. 16-bit ones), then with all chroma cleared (1 component)."""
+    rng = np.random.default_rng(seed)
+    rgb = gz.synthetic_frame(seed, w, h)
+    cmp = gz.ButteraugliComparator(w, h, rgb, 1.0)
+    for trial in range(4):
+        hi = (8, 40, 300, 2000)[trial]
+        quant = rng.integers(1, hi, size=(3, 64)).astype(np.int32)
+        co = _quantized(gz, rgb, w, h, quant)
+        if trial == 3:
+            co[1:] = 0
+        dev = cmp.write_jpeg(co.reshape(-1), quant)
+        host = gz.write_jpeg_host(co.reshape(-1), quant, w, h)
+        assert dev == host, "trial %d: %d vs %d bytes" % (trial, len(dev), len(host))
+
+
 def _jpeg_sha(gz, rgb, w, h, q):
     data, stats = gz.process(rgb, w, h, gz.Params.for_quality(q), return_stats=True)
     return hashlib.sha256(data).hexdigest(), stats
