@@ -349,6 +349,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
   alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
   alloc(reinterpret_cast<void**>(&e->d_zero_count_), static_cast<size_t>(e->nb_) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_zero_order_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4);
   alloc(reinterpret_cast<void**>(&e->d_cand_idx_), static_cast<size_t>(e->nb_) * 192);
   alloc(reinterpret_cast<void**>(&e->d_cand_err_), static_cast<size_t>(e->nb_) * 192 * 4);
@@ -414,7 +415,7 @@ Engine::~Engine() {
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
-                  d_delta_val_, d_zero_count_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
+                  d_delta_val_, d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -720,9 +721,10 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
-                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_));
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
@@ -736,9 +738,10 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
-                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_));
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   GZ_TIMED("scan_counts", k_scan_counts<<<1, 1024, 0, s>>>(d_zero_count_, nb_, d_zero_off_));
   GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 255) / 256, 256, 0, s>>>(
       static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nb_, limit, d_cand_idx_, d_cand_err_));

@@ -148,6 +148,7 @@ class Engine {
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
   int* d_zero_count_ = nullptr;    // [blocks] kept entries per block
+  int* d_zero_order_ = nullptr;    // [blocks] zeroing-search processing order
   int* d_zero_off_ = nullptr;      // [blocks + 1] their offsets
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
