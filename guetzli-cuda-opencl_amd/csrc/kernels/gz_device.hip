@@ -135,6 +135,21 @@ void BuildTables(GzTables* t) {
   BuildBlur(14.2644604355f, 0.0f, &t->blur[kSigMaskY]);
   BuildBlur(4.53358927369f, 0.0f, &t->blur[kSigMaskB]);
   BuildBlur(8.8510880283f, 0.03027655136f, &t->blur[kSigDiffmap]);
+  // blur_scale() of the sigma-1.1 blur at each position of an 8-pixel axis
+  // (the 8x8-local opsin of SwitchBlock / CompareBlock); same float sum and
+  // double normalisation as the device function
+  {
+    const BlurSpec& b = t->blur[kSigOpsin];
+    for (int pos = 0; pos < 8; ++pos) {
+      const int minx = pos < b.radius ? 0 : pos - b.radius;
+      const int maxx = (8 < pos + b.radius + 1 ? 8 : pos + b.radius + 1) - 1;
+      float weight = 0.0f;
+      for (int j = minx; j <= maxx; ++j) weight += b.taps[j - pos + b.radius];
+      weight = static_cast<float>((1.0 - static_cast<double>(b.border_ratio)) * weight +
+                                  static_cast<double>(b.border_ratio * b.weight_no_border));
+      t->opsin8_scale[pos] = static_cast<float>(1.0 / static_cast<double>(weight));
+    }
+  }
 }
 
 std::mutex g_tab_mu;
@@ -717,18 +732,42 @@ bool Engine::StartBlockComparisons(float* mask_scale_host) {
   return true;
 }
 
+// Debug knob (GZ_BZ_LDS_PAD bytes of unused dynamic LDS) to probe how the
+// zeroing search's speed depends on occupancy.
+static size_t BzLdsPad() {
+  static const size_t pad = getenv("GZ_BZ_LDS_PAD") ? static_cast<size_t>(atoi(getenv("GZ_BZ_LDS_PAD"))) : 0;
+  return pad;
+}
+
 bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  unsigned long long* timers = nullptr;
+  if (getenv("GZ_ZEROING_TIMERS")) {  // debug: per-phase cycle totals on stderr
+    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&timers), 16 * 8));
+    GZ_HIP(hipMemsetAsync(timers, 0, 16 * 8, s));
+    GZ_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_bz_timers), &timers, sizeof(timers), 0,
+                                  hipMemcpyHostToDevice, s));
+  }
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
-  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
+  if (timers) {
+    unsigned long long t[16];
+    GZ_HIP(hipMemcpy(t, timers, sizeof(t), hipMemcpyDeviceToHost));
+    unsigned long long* null_ptr = nullptr;
+    GZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bz_timers), &null_ptr, sizeof(null_ptr)));
+    GZ_HIP(hipFree(timers));
+    fprintf(stderr, "zeroing phase cycles (lane 0, summed over blocks; [15] = evaluations):");
+    for (int i = 0; i < 16; ++i) fprintf(stderr, " %d:%llu", i, t[i]);
+    fprintf(stderr, "\n");
+  }
   return true;
 }
 
@@ -739,7 +778,7 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
-  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+  GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   GZ_TIMED("scan_counts", k_scan_counts<<<1, 1024, 0, s>>>(d_zero_count_, nb_, d_zero_off_));

@@ -79,6 +79,7 @@ struct GzTables {
   double block_csf_d[37];                          // butteraugli.cc:157-198
   float zeroing_csf[192];                          // order.inc:3
   int idct[64];                                    // idct.cc:29-38
+  float opsin8_scale[8];  // border scales of the sigma-1.1 blur on an 8-wide axis (8x8 opsin)
   BlurSpec blur[kNumSigmas];
 };
 
