@@ -617,7 +617,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
-  GZ_TIMED("block_diff", k_block_diff<<<(static_cast<unsigned>(rn) + 63) / 64, 64, 0, s>>>(
+  GZ_TIMED("block_diff", k_block_diff<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), 256, 0, s>>>(
       d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_));
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
