@@ -197,8 +197,8 @@ int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram
   return ncomp;
 }
 
-bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
-                     bool strip_metadata, std::string* out, std::string* err) {
+bool DeviceEncodeJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                      bool strip_metadata, std::string* prologue, size_t* size, std::string* err) {
   JpegHistogram dc_h[3], ac_h[3];
   const int ncomp = DeviceJpegHistograms(e, q, dc_h, ac_h, err);
   if (ncomp < 0) return false;
@@ -207,8 +207,8 @@ bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], con
   hdr.com_data = meta.com_data;
   JpegHeaderFor(w, h, q, ncomp, &hdr);
   HuffCodeTable dc_tab[3], ac_tab[3];
-  out->clear();
-  if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, out)) {
+  prologue->clear();
+  if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, prologue)) {
     if (err) *err = "jpeg header";
     return false;
   }
@@ -221,14 +221,39 @@ bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], con
       codes.dc_code[c][i] = static_cast<uint16_t>(dc_tab[c].code[i]);
       codes.ac_code[c][i] = static_cast<uint16_t>(ac_tab[c].code[i]);
     }
-  const uint8_t* bytes = nullptr;
-  uint64_t nbits = 0;
-  if (!e->JpegScan(ncomp, codes, &bytes, &nbits)) {
+  uint64_t nbits = 0, ff = 0;
+  if (!e->JpegScan(ncomp, codes, &nbits, &ff)) {
     if (err) *err = e->error();
     return false;
   }
-  AppendStuffedScan(bytes, nbits, out);
+  // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
+  *size = prologue->size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
   return true;
+}
+
+bool DeviceFetchJpeg(Engine* e, bool kept, const std::string& prologue, size_t size,
+                     std::string* out, std::string* err) {
+  const uint8_t* bytes = nullptr;
+  uint64_t nbits = 0;
+  if (!e->JpegFetch(kept, &bytes, &nbits)) {
+    if (err) *err = e->error();
+    return false;
+  }
+  *out = prologue;
+  AppendStuffedScan(bytes, nbits, out);
+  if (out->size() != size) {  // the device's size prediction is what the search scored
+    if (err) *err = "device JPEG size prediction mismatch";
+    return false;
+  }
+  return true;
+}
+
+bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                     bool strip_metadata, std::string* out, std::string* err) {
+  std::string prologue;
+  size_t size = 0;
+  return DeviceEncodeJpeg(e, w, h, q, meta, strip_metadata, &prologue, &size, err) &&
+         DeviceFetchJpeg(e, false, prologue, size, out, err);
 }
 
 int HipButteraugliComparator::DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3],
@@ -241,6 +266,26 @@ bool HipButteraugliComparator::DeviceWriteJpeg(const CoeffImage& img, const Jpeg
                                                bool strip_metadata, std::string* out) {
   if (!SyncCoeffs(img)) return false;
   return gz::DeviceWriteJpeg(engine_.get(), w_, h_, img.quant, meta, strip_metadata, out, &err_);
+}
+
+bool HipButteraugliComparator::DeviceEncode(const CoeffImage& img, const JpegData& meta,
+                                            bool strip_metadata, size_t* size) {
+  if (!SyncCoeffs(img)) return false;
+  if (!DeviceEncodeJpeg(engine_.get(), w_, h_, img.quant, meta, strip_metadata, &cur_prologue_,
+                        &cur_size_, &err_))
+    return false;
+  *size = cur_size_;
+  return true;
+}
+
+void HipButteraugliComparator::DeviceKeepEncoded() {
+  engine_->JpegKeep();
+  kept_prologue_.swap(cur_prologue_);
+  kept_size_ = cur_size_;
+}
+
+bool HipButteraugliComparator::DeviceFetchKept(std::string* out) {
+  return DeviceFetchJpeg(engine_.get(), true, kept_prologue_, kept_size_, out, &err_);
 }
 
 bool HipButteraugliComparator::StartBlockComparisons() {
@@ -605,14 +650,16 @@ class Processor {
     pending_.clear();
     if (cmp_->HasDeviceWriter()) {
       // entropy coded on the device from its resident copy (sub-ms), no
-      // helper thread needed
-      if (!cmp_->DeviceWriteJpeg(img, jpg, params_.clear_metadata, &pending_)) return Fail(err);
+      // helper thread needed; the bytes stay there unless kept
+      if (!cmp_->DeviceEncode(img, jpg, params_.clear_metadata, &pending_size_)) return Fail(err);
       has_pending_ = true;
+      pending_device_ = true;
       const double dt = Since(t0);
       res_->seconds_write += dt;
       res_->detail["write_device_s"] += dt;
       return true;
     }
+    pending_device_ = false;
     StageCoeffImage(img, jpg, scratch_.get());
     writer_ = std::thread([this] {
       const auto t = Clock::now();
@@ -637,14 +684,30 @@ class Processor {
       res_->detail["write_encode_s"] += encode_s_;
     }
     has_pending_ = false;
+    if (pending_device_) {
+      MaybeOutputDevice(pending_size_);
+      return pending_size_;
+    }
     MaybeOutput(pending_);
     return pending_.size();
   }
+  // processor.cc:899-904 (the score depends on the size alone)
   void MaybeOutput(const std::string& encoded) {
     const double score = cmp_->ScoreOutputSize(static_cast<int>(encoded.size()));
     if (score < final_score_ || final_score_ < 0) {
       res_->jpeg = encoded;
       final_score_ = score;
+      best_size_ = encoded.size();
+      kept_on_device_ = false;
+    }
+  }
+  void MaybeOutputDevice(size_t size) {
+    const double score = cmp_->ScoreOutputSize(static_cast<int>(size));
+    if (score < final_score_ || final_score_ < 0) {
+      cmp_->DeviceKeepEncoded();
+      final_score_ = score;
+      best_size_ = size;
+      kept_on_device_ = true;
     }
   }
   bool TryQuantMatrix(const JpegData& jpg_in, float target_mul, const int q[3][kDCTBlockSize],
@@ -665,6 +728,10 @@ class Processor {
   std::thread writer_;
   std::string pending_;
   bool has_pending_ = false;
+  bool pending_device_ = false;
+  size_t pending_size_ = 0;
+  bool kept_on_device_ = false;  // the best candidate so far is the device's kept slot
+  size_t best_size_ = 0;
   double encode_s_ = 0.0;
   double final_score_ = -1;
 };
@@ -772,8 +839,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   bool first_up_iter = true;
   for (int direction : {1, -1}) {
     for (;;) {
-      if (stop_early) FlushOutput();  // res_->jpeg must be current
-      if (stop_early && direction == -1 && prev_size > 1.01 * res_->jpeg.size()) break;
+      if (stop_early) FlushOutput();  // best_size_ must be current
+      if (stop_early && direction == -1 && prev_size > 1.01 * best_size_) break;
       const auto tb = Clock::now();
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
@@ -935,6 +1002,7 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
       for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
   if (!cmp_->QuantizeFromOriginal(best_q, &img)) return device_error();
   if (!SelectFrequencyMasking(jpg, &img, 7, 1.0, false, err)) return GZ_ERR_DEVICE;
+  if (kept_on_device_ && !cmp_->DeviceFetchKept(&res_->jpeg)) return device_error();
   return GZ_OK;
 }
 

@@ -58,6 +58,16 @@ class Comparator {
                                std::string* out) {
     return false;
   }
+  // The search's per-candidate form of it: the candidate stays on the device
+  // and only its file size comes back; DeviceKeepEncoded marks the last
+  // encoded candidate as the one to keep (the next encode may overwrite any
+  // other), DeviceFetchKept returns the kept candidate's bytes.
+  virtual bool DeviceEncode(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                            size_t* size) {
+    return false;
+  }
+  virtual void DeviceKeepEncoded() {}
+  virtual bool DeviceFetchKept(std::string* out) { return false; }
   // DC / AC histograms of img as SaveToJpegData stores it (comps at or above
   // the returned count cleared) from the device copy; -1 if unsupported.
   virtual int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) {
@@ -89,6 +99,12 @@ void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int 
 // image w x h, metadata of meta) entropy coded on the device.
 bool DeviceWriteJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
                      bool strip_metadata, std::string* out, std::string* err);
+// The same leaving the scan in the engine's current JPEG slot: *prologue
+// (headers), *size the file size; DeviceFetchJpeg assembles a slot's file.
+bool DeviceEncodeJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                      bool strip_metadata, std::string* prologue, size_t* size, std::string* err);
+bool DeviceFetchJpeg(Engine* e, bool kept, const std::string& prologue, size_t size,
+                     std::string* out, std::string* err);
 // The histogram stage of it alone (for the search back end's size model).
 int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram dc[3],
                          JpegHistogram ac[3], std::string* err);
@@ -113,6 +129,10 @@ class HipButteraugliComparator : public Comparator {
   bool HasDeviceWriter() const override { return true; }
   bool DeviceWriteJpeg(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                        std::string* out) override;
+  bool DeviceEncode(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                    size_t* size) override;
+  void DeviceKeepEncoded() override;
+  bool DeviceFetchKept(std::string* out) override;
   int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) override;
   double ScoreOutputSize(int size) const override;
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }
@@ -145,6 +165,8 @@ class HipButteraugliComparator : public Comparator {
   float distance_ = 0.0f;
   std::vector<float> block_max_;
   CoeffCursor device_;  // what the device copy of the coefficients reflects
+  std::string cur_prologue_, kept_prologue_;  // headers of the encoded / kept candidates
+  size_t cur_size_ = 0, kept_size_ = 0;
   std::string err_;
 };
 

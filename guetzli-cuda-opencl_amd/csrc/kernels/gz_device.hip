@@ -25,6 +25,7 @@ __constant__ GzTables c_tab;
 }
 
 #include "butteraugli_kernels.inc"
+#include "scan_kernels.inc"
 #include "block_zeroing.inc"
 #include "coeff_kernels.inc"
 #include "jpeg_kernels.inc"
@@ -366,6 +367,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_zero_count_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_zero_order_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_zero_nnz_), static_cast<size_t>(e->nb_) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_zero_bins_), 2 * kOrderBins * 4);
+  alloc(reinterpret_cast<void**>(&e->d_scan_sums_), (static_cast<size_t>(e->nb_) / kScanChunk + 1) * 4);
   alloc(reinterpret_cast<void**>(&e->d_cand_idx_), static_cast<size_t>(e->nb_) * 192);
   alloc(reinterpret_cast<void**>(&e->d_cand_err_), static_cast<size_t>(e->nb_) * 192 * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4) != hipSuccess)
@@ -380,7 +384,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jbitoff_), static_cast<size_t>(e->nb_ + 1) * 4);
   // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
   e->jwords_cap_ = static_cast<size_t>(e->nb_) * 160 + 16;
-  alloc(reinterpret_cast<void**>(&e->d_jwords_), e->jwords_cap_ * 4);
+  alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
+  alloc(reinterpret_cast<void**>(&e->d_jwords_[1]), e->jwords_cap_ * 4);
+  alloc(reinterpret_cast<void**>(&e->d_jinfo_), 16);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 16) != hipSuccess)
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodeTables)) != hipSuccess)
@@ -431,7 +437,8 @@ Engine::~Engine() {
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
                   d_delta_val_, d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
-                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_};
+                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
+                  d_zero_bins_, d_scan_sums_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
@@ -739,6 +746,27 @@ static size_t BzLdsPad() {
   return pad;
 }
 
+// offsets[0..n] = exclusive prefix sums of the device counts[0..n), on the stream.
+bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (n > nb_) return Fail("ScanCounts size", 0);
+  const unsigned chunks = static_cast<unsigned>((n + kScanChunk - 1) / kScanChunk);
+  GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
+                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets)));
+  return true;
+}
+
+// d_zero_order_ = blocks by decreasing non-zero AC count (k_block_nnz / k_order_scatter).
+bool Engine::OrderBlocks(int comp_mask) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  const unsigned groups = static_cast<unsigned>((nb_ + kOrderGroup - 1) / kOrderGroup);
+  GZ_HIP(hipMemsetAsync(d_zero_bins_, 0, 2 * kOrderBins * 4, s));
+  GZ_TIMED("order_blocks", (k_block_nnz<<<groups, 256, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_nnz_, d_zero_bins_),
+                            k_order_scatter<<<groups, 256, 0, s>>>(d_zero_nnz_, nb_, d_zero_bins_,
+                                                                 d_zero_bins_ + kOrderBins, d_zero_order_)));
+  return true;
+}
+
 bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
@@ -750,7 +778,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
                                   hipMemcpyHostToDevice, s));
   }
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
-  GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
+  if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
@@ -777,12 +805,12 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
-  GZ_TIMED("order_blocks", k_order_blocks<<<1, 1024, 0, s>>>(d_cur_, nb_, comp_mask, d_zero_order_));
+  if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
-  GZ_TIMED("scan_counts", k_scan_counts<<<1, 1024, 0, s>>>(d_zero_count_, nb_, d_zero_off_));
-  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 255) / 256, 256, 0, s>>>(
+  if (!ScanCounts(d_zero_count_, nb_, d_zero_off_, "scan_counts")) return false;
+  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 3) / 4, 256, 0, s>>>(
       static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nb_, limit, d_cand_idx_, d_cand_err_));
   GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nb_ + 1) * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
@@ -830,7 +858,7 @@ bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) 
   return true;
 }
 
-bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, const uint8_t** bytes, uint64_t* nbits) {
+bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
@@ -839,28 +867,43 @@ bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, const uint8_t** by
   *h_jcodes_ = codes;
   GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodeTables), hipMemcpyHostToDevice, s));
   const JpegCodeTables* dc = static_cast<const JpegCodeTables*>(d_jcodes_);
-  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<(nb_ + 255) / 256, 256, 0, s>>>(d_jzz_, d_jmask_, nb_, ncomp, dc,
-                                                                    d_jbitlen_));
-  GZ_TIMED("jpeg_scan", k_scan_counts<<<1, 1024, 0, s>>>(d_jbitlen_, nb_, d_jbitoff_));
+  uint32_t* words = d_jwords_[jslot_];
+  const unsigned mcu_groups = static_cast<unsigned>((nb_ + 3) / 4);
+  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_));
+  if (!ScanCounts(d_jbitlen_, nb_, d_jbitoff_, "jpeg_scan")) return false;
+  // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any scan)
+  GZ_HIP(hipMemsetAsync(d_jinfo_, 0, 4, s));
+  GZ_TIMED("jpeg_emit", (k_zero_words<<<512, 256, 0, s>>>(d_jbitoff_ + nb_, words),
+                         k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
+                         k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_)));
   GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jbitoff_ + nb_, 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 3, d_jinfo_, 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   const uint64_t total = h_jhist_[6 * 256 + 2];
-  const size_t words = static_cast<size_t>((total + 31) / 32);
-  if (words + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
-  GZ_HIP(hipMemsetAsync(d_jwords_, 0, (words + 1) * 4, s));
-  GZ_TIMED("jpeg_emit", k_jpeg_emit<<<(nb_ + 255) / 256, 256, 0, s>>>(d_jzz_, d_jmask_, nb_, ncomp, dc,
-                                                                    d_jbitoff_, d_jwords_));
-  if (words * 4 > h_jbytes_cap_) {
+  if ((total + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
+  jnbits_[jslot_] = total;
+  *nbits = total;
+  *ff = h_jhist_[6 * 256 + 3];
+  return true;
+}
+
+bool Engine::JpegFetch(bool kept, const uint8_t** bytes, uint64_t* nbits) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  const int slot = kept ? jslot_ ^ 1 : jslot_;
+  const uint64_t total = jnbits_[slot];
+  const size_t nbytes = static_cast<size_t>((total + 7) / 8);
+  if (nbytes + 8 > h_jbytes_cap_) {
     if (h_jbytes_) GZ_HIP(hipHostFree(h_jbytes_));
     h_jbytes_ = nullptr;
     h_jbytes_cap_ = 0;
-    const size_t cap = words * 4 + words + 4096;
+    const size_t cap = nbytes + nbytes / 4 + 4096;
     GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_jbytes_), cap));
     h_jbytes_cap_ = cap;
   }
-  if (words) GZ_HIP(hipMemcpyAsync(h_jbytes_, d_jwords_, words * 4, hipMemcpyDeviceToHost, s));
+  if (nbytes) GZ_HIP(hipMemcpyAsync(h_jbytes_, d_jwords_[slot], nbytes, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
-  ProfFlush();
   *bytes = h_jbytes_;
   *nbits = total;
   return true;

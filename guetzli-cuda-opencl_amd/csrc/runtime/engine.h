@@ -93,10 +93,17 @@ class Engine {
   // per-iteration JPEG of the search).  JpegStage: quantized zigzag
   // coefficients, symbol histograms hist[comp*2 + {0:DC, 1:AC}][256] (plain
   // counts) and the number of non-zero chroma coefficients.  JpegScan: the
-  // scan bitstream of the staged image for `ncomp` components with `codes`;
-  // *bytes (MSB-first, valid until the next call) holds *nbits bits.
+  // scan bitstream of the staged image for `ncomp` components with `codes`
+  // into the current slot (padded to a byte with ones): *nbits bits, *ff
+  // bytes 0xff (the stuffing doubles them).  Two slots: JpegKeep makes the
+  // current one the kept one (the next scan overwrites the other);
+  // JpegFetch copies a slot's bytes (MSB-first, valid until the next call).
   bool JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz);
-  bool JpegScan(int ncomp, const JpegCodeTables& codes, const uint8_t** bytes, uint64_t* nbits);
+  bool JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff);
+  void JpegKeep() { jslot_ ^= 1; }
+  bool JpegFetch(bool kept, const uint8_t** bytes, uint64_t* nbits);
+  bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
+  bool OrderBlocks(int comp_mask);
 
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
@@ -150,6 +157,9 @@ class Engine {
   int* d_zero_count_ = nullptr;    // [blocks] kept entries per block
   int* d_zero_order_ = nullptr;    // [blocks] zeroing-search processing order
   int* d_zero_off_ = nullptr;      // [blocks + 1] their offsets
+  int* d_zero_nnz_ = nullptr;      // [blocks] non-zero AC counts (processing order)
+  int* d_zero_bins_ = nullptr;     // [2][193] count histogram, scatter cursors
+  int* d_scan_sums_ = nullptr;     // [blocks / kScanChunk + 1] chunk totals
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
   int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
@@ -159,7 +169,10 @@ class Engine {
   void* d_jcodes_ = nullptr;       //   JpegCodeTables
   int* d_jbitlen_ = nullptr;       //   [blocks]
   int* d_jbitoff_ = nullptr;       //   [blocks + 1]
-  uint32_t* d_jwords_ = nullptr;   //   scan bitstream
+  uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
+  uint64_t jnbits_[2] = {0, 0};
+  int jslot_ = 0;                  // current slot (kept = jslot_ ^ 1)
+  int* d_jinfo_ = nullptr;         //   0xff count
   size_t jwords_cap_ = 0;
   uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + total bits
   JpegCodeTables* h_jcodes_ = nullptr;
