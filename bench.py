@@ -56,10 +56,7 @@ def stage_bytes_per_px():
     s["lowfreq_blur_h"] = 6 * 4 + 6 * 4 / 4.0
     s["lowfreq_blur_v"] = 6 * 4 / 4.0 + 6 * 4 / 16.0
     s["low_freq"] = 6 * 4 / 16.0 + 2 * 3 * 4 / 9.0
-    s["mask_diff_precompute"] = 6 * 4 + 3 * 4
-    s["mask_average5x5"] = 3 * 4 + 3 * 4
-    s["mask_min4_v"] = 3 * 4 + 3 * 4
-    s["mask_min4_h"] = 3 * 4 + 3 * 4
+    s["mask_front"] = 6 * 4 + 3 * 4                 # S9-S11 fused: 6 planes -> 3
     s["mask_blur_h"] = 3 * 4 + 4 * (1 / 3.0 + 1 / 4.0 + 1.0)
     s["mask_blur_v"] = 4 * (1 / 3.0 + 1 / 4.0 + 1.0) + 4 * (1 / 9.0 + 1 / 16.0 + 1.0)
     s["combine"] = (3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 4) / 9.0
@@ -75,8 +72,7 @@ def stage_bytes_per_px():
 # S14/S15) are timed whole, so the extra fused work only lowers the figure.
 BLUR_MASK_BYTES_PER_PX = 272.0
 BLUR_MASK_STAGES = ("opsin", "edge_blur", "lowfreq_blur_h",
-                    "lowfreq_blur_v", "mask_diff_precompute", "mask_average5x5", "mask_min4_v",
-                    "mask_min4_h", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
+                    "lowfreq_blur_v", "mask_front", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
@@ -85,8 +81,7 @@ STAGE_SYMBOL = {
     "mhic": "gz::k_mhic(", "edge_blur": "void gz::k_blur2d<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h_tiled<3,",
     "lowfreq_blur_v": "void gz::k_blur_v<3>(", "low_freq": "gz::k_low_freq(",
-    "mask_diff_precompute": "gz::k_diff_precompute(", "mask_average5x5": "gz::k_average5x5(",
-    "mask_min4_v": "gz::k_min4_v(", "mask_min4_h": "gz::k_min4_h(",
+    "mask_front": "gz::k_mask_front(",
     "mask_blur_h": "void gz::k_blur_h_tiled<4,", "mask_blur_v": "void gz::k_blur_v<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h_tiled<5,",
     "diffmap_blur_v": "void gz::k_blur_v<5>(", "diffmap_final": "gz::k_diffmap_final(",

@@ -553,10 +553,10 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
 
 bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  GZ_TIMED("mask_diff_precompute", k_diff_precompute<<<PixGrid(w_, h_), 256, 0, s>>>(xyb0, xyb1, w_, h_, d_ma_));
-  GZ_TIMED("mask_average5x5", k_average5x5<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_));
-  GZ_TIMED("mask_min4_v", k_min4_v<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_mb_, w_, h_, d_ma_));
-  GZ_TIMED("mask_min4_h", k_min4_h<<<PixGrid(w_, h_, 3), 256, 0, s>>>(d_ma_, w_, h_, d_mb_));
+  {
+    const int tx = (w_ + kMfTX - 1) / kMfTX, ty = (h_ + kMfTY - 1) / kMfTY;
+    GZ_TIMED("mask_front", (k_mask_front<kMfTX, kMfTY><<<dim3(tx * ty, 3), 256, 0, s>>>(xyb0, xyb1, w_, h_, tx, d_mb_)));
+  }
   BlurPlanes bp{};
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_mb_ + c * n_;
