@@ -48,8 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def stage_bytes_per_px():
     s = {}
     s["coeffs_to_linear"] = 3 * 2 + 3 * 4          # int16 coeffs -> 3 f32 planes
-    s["opsin"] = 3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 3 * 4  # S1 blur (3->3) + S2 transform (6->3)
-    s["mhic"] = 6 * 4 + 6 * 4
+    s["opsin_mhic"] = 3 * 4 + 3 * 4 + 6 * 4          # S1-S3 fused: linear + ref XYB -> m0, m1
     s["edge_blur"] = 6 * 4 + 6 * 4                  # S4: 6 separable blurs, 6 -> 6
     s["edge_map"] = 6 * 4 + 3 * 4 / 9.0
     s["block_diff"] = 6 * 4 + 6 * 4 / 9.0
@@ -68,17 +67,17 @@ def stage_bytes_per_px():
 
 # The "blur+mask pass" of BASELINE.json / SURVEY.md 8(d): blurs S1, S4, S7,
 # S16 and the mask chain S9-S13, 272 algorithmic B/px.  Kernels that carry
-# those stages (the opsin kernel also does the S2 transform, combine the S13 LUTs with
+# those stages (the opsin kernel also does the S2 transform and S3, combine the S13 LUTs with
 # S14/S15) are timed whole, so the extra fused work only lowers the figure.
 BLUR_MASK_BYTES_PER_PX = 272.0
-BLUR_MASK_STAGES = ("opsin", "edge_blur", "lowfreq_blur_h",
+BLUR_MASK_STAGES = ("opsin_mhic", "edge_blur", "lowfreq_blur_h",
                     "lowfreq_blur_v", "mask_front", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
 STAGE_SYMBOL = {
-    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin": "gz::k_opsin2d(",
-    "mhic": "gz::k_mhic(", "edge_blur": "void gz::k_blur2d<2>(", "edge_map": "gz::k_edge_map(",
+    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_mhic": "gz::k_opsin_mhic(",
+    "edge_blur": "void gz::k_blur2d<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h_tiled<3,",
     "lowfreq_blur_v": "void gz::k_blur_v<3>(", "low_freq": "gz::k_low_freq(",
     "mask_front": "gz::k_mask_front(",

@@ -592,15 +592,15 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // S0: candidate coefficients -> linear RGB
   GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_));
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
-  // S1/S2: opsin dynamics (blur + transform fused)
+  // S1-S3: opsin dynamics (blur + transform) and high intensity change
+  // masking, fused
   {
-    const int tx = (w_ + kOpTX - 1) / kOpTX, ty = (h_ + kOpTY - 1) / kOpTY;
-    GZ_TIMED("opsin", k_opsin2d<<<tx * ty, 256, 0, s>>>(d_lin_, w_, h_, tx, d_xyb_, d_scales_,
-                                                          scale_stride_));
+    const int tx = (w_ + kOmTX - 1) / kOmTX, ty = (h_ + kOmTY - 1) / kOmTY;
+    float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
+    GZ_TIMED("opsin_mhic", k_opsin_mhic<<<tx * ty, 256, 0, s>>>(d_lin_, d_ref_xyb_, w_, h_, tx, d_m0_, d_m1_,
+                                                                  xyb_dbg, d_scales_, scale_stride_));
+    if (xyb_dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   }
-  if (dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
-  // S3: high intensity change masking
-  GZ_TIMED("mhic", k_mhic<<<PixGrid(w_, h_), 256, 0, s>>>(d_ref_xyb_, d_xyb_, w_, h_, d_m0_, d_m1_));
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
   if (dbg && !d2h(dbg->mhic1, d_m1_, 3 * n)) return false;
   // S4/S5: edge detector map (6 step-1 blurs of radius <= 3, fused 2-D)
