@@ -34,6 +34,11 @@ enum SigmaId : int {
 // 60-69: radius = max(1, int(2.25f * sigma)), step = max(1, int(sigma / 3))),
 // so that tap loops unroll with the taps in scalar registers.  Checked
 // against the host-built table when an engine is created.
+// Two f32 lanes in one register pair: arithmetic on it compiles to the
+// packed v_pk_mul_f32 / v_pk_add_f32 (two correctly rounded f32 results per
+// instruction; -ffp-contract=off keeps them separate, as the scalar code).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int kSig> struct BlurGeom;
 template <> struct BlurGeom<kSigOpsin> { static constexpr int R = 2, STEP = 1; };
 template <> struct BlurGeom<kSigEdgeX> { static constexpr int R = 3, STEP = 1; };
