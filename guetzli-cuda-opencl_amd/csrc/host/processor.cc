@@ -904,8 +904,46 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       const size_t n_order = global_order.size();
       double codes_s = 0.0;
       int n_codes = 0;
+      // Prefetch window: when the lazy sort hands out a new sorted chunk, the
+      // chunk's per-block state is touched ahead of the (serial) changes in
+      // three dependent passes -- block bookkeeping, then the candidate byte,
+      // then the coefficient block and its non-zero mask -- so the cache
+      // misses of a chunk overlap instead of chaining.  Values are only
+      // prefetched; the loop below reads them as before.
+      size_t prefetched = 0;
+      auto prefetch_chunk = [&](size_t lo, size_t hi) {
+        for (size_t j = lo; j < hi; ++j) {
+          const int b = global_order[j].first;
+          __builtin_prefetch(&last_indexes[b]);
+          __builtin_prefetch(&offsets[b]);
+        }
+        for (size_t j = lo; j < hi; ++j) {
+          const int b = global_order[j].first;
+          const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
+          const int ci = off + last_indexes[b] + std::min(direction, 0);
+          if (ci >= 0 && ci < static_cast<int>(cand.size())) __builtin_prefetch(&cand[ci]);
+        }
+        for (size_t j = lo; j < hi; ++j) {
+          const int b = global_order[j].first;
+          const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
+          const int ci = off + last_indexes[b] + std::min(direction, 0);
+          if (ci < 0 || ci >= static_cast<int>(cand.size())) continue;
+          const int c = cand[ci] / kDCTBlockSize;
+          __builtin_prefetch(img->block(c, b), 1);
+          __builtin_prefetch(&acm.nz[static_cast<size_t>(c) * num_blocks + b], 1);
+        }
+      };
+      double sort_s = 0.0;
       for (size_t i = 0; i < n_order; ++i) {
-        if (i >= sorter.sorted()) sorter.EnsureSorted(i);
+        if (i >= sorter.sorted()) {
+          const auto ts = Clock::now();
+          sorter.EnsureSorted(i);
+          sort_s += Since(ts);
+        }
+        if (i >= prefetched) {
+          prefetched = std::max(sorter.sorted(), i + 1);
+          prefetch_chunk(i, std::min(prefetched, n_order));
+        }
         const int bix = global_order[i].first;
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
@@ -938,6 +976,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       }
       res_->detail["backend_changes_s"] += Since(tc);
       res_->detail["backend_codes_s"] += codes_s;
+      res_->detail["backend_sort_s"] += sort_s;
       res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += changed_coeffs;
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;

@@ -554,8 +554,10 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
 bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   {
-    const int tx = (w_ + kMfTX - 1) / kMfTX, ty = (h_ + kMfTY - 1) / kMfTY;
-    GZ_TIMED("mask_front", (k_mask_front<kMfTX, kMfTY><<<dim3(tx * ty, 3), 256, 0, s>>>(xyb0, xyb1, w_, h_, tx, d_mb_)));
+    const int strips = (w_ + kMsCols - 1) / kMsCols, segs = (h_ + kMsRows - 1) / kMsRows;
+    const int waves = 3 * strips * segs;
+    GZ_TIMED("mask_front", k_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(xyb0, xyb1, w_, h_, strips, segs,
+                                                                          kMsRows, d_mb_));
   }
   BlurPlanes bp{};
   for (int c = 0; c < 3; ++c) {
@@ -616,10 +618,12 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       b2.sig[3 + c] = sig;
     }
     b2.nplanes = 6;
-    b2.tiles_x = (w_ + kB2TX - 1) / kB2TX;
-    b2.tiles_y = (h_ + kB2TY - 1) / kB2TY;
-    GZ_TIMED("edge_blur", k_blur2d<kBlurEdge><<<b2.nplanes * b2.tiles_x * b2.tiles_y, 256, 0, s>>>(
-        b2, w_, h_, d_scales_, scale_stride_));
+    const int rows = kBsRows;
+    b2.tiles_x = (w_ + kBsCols - 1) / kBsCols;
+    b2.tiles_y = (h_ + rows - 1) / rows;
+    const int waves = b2.nplanes * b2.tiles_x * b2.tiles_y;
+    GZ_TIMED("edge_blur", k_blur_stream<kBlurEdge><<<(waves + 3) / 4, 256, 0, s>>>(
+        b2, w_, h_, rows, d_scales_, scale_stride_));
   }
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;

@@ -1,7 +1,6 @@
 #!/bin/bash
-# A/B of an environment switch on the isolated per-kernel stage times:
-#   GZ_AB_VAR=NAME GZ_AB_FILTER=regex bash tools/ab_probe.sh
+# A/B of an environment switch on the isolated per-kernel stage times
+# (unset vs =1):  GZ_AB_VAR=NAME GZ_AB_FILTER=regex bash tools/ab_probe.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for v in "" 1; do
-  env ${GZ_AB_VAR}=$v timeout -k 10 120 python tools/stage_times.py 2>&1 | grep -E "${GZ_AB_FILTER:-compare_pass}" | sed "s/^/[${GZ_AB_VAR}=$v] /"
-done
+env -u ${GZ_AB_VAR} timeout -k 10 120 python tools/stage_times.py ${GZ_AB_ARGS:-} 2>&1 | grep -E "${GZ_AB_FILTER:-compare_pass}" | sed "s/^/[${GZ_AB_VAR} unset] /"
+env ${GZ_AB_VAR}=1 timeout -k 10 120 python tools/stage_times.py ${GZ_AB_ARGS:-} 2>&1 | grep -E "${GZ_AB_FILTER:-compare_pass}" | sed "s/^/[${GZ_AB_VAR}=1] /"

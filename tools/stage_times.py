@@ -31,9 +31,11 @@ def main():
     gz.process(rgb, args.width, args.height, params)
     wall = time.perf_counter() - t0
     gz.profile_enable(False)
+    detail = gz.last_process_detail()
     p = gz.profile_read()
     tot = sum(v[1] for v in p.values())
     print(f"frame {args.width}x{args.height}: wall {wall * 1e3:.1f} ms, timed regions {tot:.2f} ms")
+    print("host detail:", {k: round(v, 4) for k, v in detail.items()})
     for k, (n, ms) in sorted(p.items(), key=lambda kv: -kv[1][1]):
         print(f"  {k:28s} {n:5d} x {ms / max(n, 1):8.4f} ms = {ms:8.3f} ms")
 
