@@ -79,11 +79,11 @@ STAGE_SYMBOL = {
     "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_mhic": "gz::k_opsin_mhic(",
     "edge_blur": "void gz::k_blur_stream<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h_tiled<3,",
-    "lowfreq_blur_v": "void gz::k_blur_v<3>(", "low_freq": "gz::k_low_freq(",
+    "lowfreq_blur_v": "void gz::k_blur_vcol<3>(", "low_freq": "gz::k_low_freq(",
     "mask_front": "gz::k_mask_stream(",
-    "mask_blur_h": "void gz::k_blur_h_tiled<4,", "mask_blur_v": "void gz::k_blur_v<4>(",
+    "mask_blur_h": "void gz::k_blur_h_tiled<4,", "mask_blur_v": "void gz::k_blur_vcol<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h_tiled<5,",
-    "diffmap_blur_v": "void gz::k_blur_v<5>(", "diffmap_final": "gz::k_diffmap_final(",
+    "diffmap_blur_v": "void gz::k_blur_vcol<5>(", "diffmap_final": "gz::k_diffmap_final(",
 }
 
 

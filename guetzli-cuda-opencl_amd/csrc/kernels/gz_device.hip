@@ -184,6 +184,39 @@ inline dim3 PackBlurGrid(BlurPlanes* bp, int planes, int w, int h, bool vertical
   }
   return dim3(bp->start[planes]);
 }
+// Wave items of k_blur_vcol: per plane (64-column group, row segment).
+inline int VColSegments(int sig, int h) {
+  switch (sig) {
+    case kSigLowFreq: return vcol_segments<kSigLowFreq>(h);
+    case kSigMaskX: return vcol_segments<kSigMaskX>(h);
+    case kSigMaskY: return vcol_segments<kSigMaskY>(h);
+    case kSigMaskB: return vcol_segments<kSigMaskB>(h);
+    default: return vcol_segments<kSigDiffmap>(h);
+  }
+}
+inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
+  bp.nplanes = planes;
+  bp.start[0] = 0;
+  for (int p = 0; p < planes; ++p) {
+    const int st = HostTables().blur[bp.sig[p]].step;
+    const int dx = (w + st - 1) / st;
+    bp.tiles[p] = (dx + 63) / 64;
+    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * VColSegments(bp.sig[p], h);
+  }
+  return dim3((bp.start[planes] + 3) / 4);
+}
+// Wave items of k_blur_h4: per plane (256-output band, row).
+inline dim3 BlurH4Grid(int w, int h, int planes, BlurPlanes& bp) {
+  bp.nplanes = planes;
+  bp.start[0] = 0;
+  for (int p = 0; p < planes; ++p) {
+    const int st = HostTables().blur[bp.sig[p]].step;
+    const int dx = (w + st - 1) / st;
+    bp.tiles[p] = (dx + 255) / 256;
+    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * h;
+  }
+  return dim3((bp.start[planes] + 3) / 4);
+}
 inline dim3 BlurHGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, false); }
 inline dim3 BlurVGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, true); }
 inline RowsPlain Rows(const BlurPlanes& bp, int w) {
@@ -565,15 +598,15 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
     bp.out[c] = d_tmp_ + c * n_;
     bp.sig[c] = kSigMaskX + c;
   }
-  const dim3 grid2 = BlurHGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("mask_blur_h", k_blur_h_tiled<kBlurMask><<<grid2, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
+  const dim3 grid2 = BlurH4Grid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_h", k_blur_h4<kBlurMask><<<grid2, 256, 0, s>>>(
+      Rows(bp, w_), bp, w_, h_, d_scales_, scale_stride_));
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  const dim3 grid3 = BlurVGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("mask_blur_v", k_blur_v<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  const dim3 grid3 = BlurVColGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_v", k_blur_vcol<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -641,9 +674,9 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     bp.sig[3 + c] = kSigLowFreq;
   }
   for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  const dim3 grid7 = BlurHGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("lowfreq_blur_h", k_blur_h_tiled<kBlurLowFreq><<<grid7, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, d_scales_, scale_stride_));
+  const dim3 grid7 = BlurH4Grid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("lowfreq_blur_h", k_blur_h4<kBlurLowFreq><<<grid7, 256, 0, s>>>(
+      Rows(bp, w_), bp, w_, h_, d_scales_, scale_stride_));
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -651,8 +684,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    const dim3 grid8 = BlurVGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-    GZ_TIMED("lowfreq_blur_v", k_blur_v<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    const dim3 grid8 = BlurVColGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("lowfreq_blur_v", k_blur_vcol<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -676,13 +709,13 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     BlurPlanes bd{};
     bd.out[0] = d_tmp_;
     bd.sig[0] = kSigDiffmap;
-    const dim3 grid9 = BlurHGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_h", k_blur_h_tiled<kBlurDiffmap><<<grid9, 256, 0, s>>>(
-        RowsDiffmap{d_resval_, rw_}, bd, wc, d_scales_, scale_stride_));
+    const dim3 grid9 = BlurH4Grid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_h", k_blur_h4<kBlurDiffmap><<<grid9, 256, 0, s>>>(
+        RowsDiffmap{d_resval_, rw_}, bd, wc, hc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    const dim3 grid10 = BlurVGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_v", k_blur_v<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
+    const dim3 grid10 = BlurVColGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_v", k_blur_vcol<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
