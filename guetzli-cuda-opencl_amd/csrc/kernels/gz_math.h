@@ -128,6 +128,17 @@ __device__ __forceinline__ BlockId xcd_block_id() {
 // Small helpers
 // ---------------------------------------------------------------------------
 
+// Lane shifts by DPP (a VALU modifier, no LDS round trip): wave_next(v) is
+// lane i+1's value in lane i, wave_prev(v) lane i-1's; the edge lane gets 0.
+// Call them with the whole wave active (outside lane-divergent branches).
+__device__ __forceinline__ float wave_next(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
+
 __device__ __forceinline__ float interp_f(const float* a, int size, float sx) {
   // InterpolateOpt, clbutter_comparator.cpp:195-210
   const float ix = fabsf(sx);
@@ -250,7 +261,10 @@ __device__ __forceinline__ float gamma_poly(float x) {
   // GammaPolynomialOpt, :861-874 (RationalPolynomialOpt :828-859)
   const float lo = 0.770000000000000f, hi = 274.579999999999984f;
   const float x01 = (x - lo) / (hi - lo);
-  const float xc = static_cast<float>(2.0 * static_cast<double>(x01) - 1.0);
+  // float(2.0 * double(x01) - 1.0) == 2.0f * x01 - 1.0f: the doubled value is
+  // exact, and the difference is exact in double unless |2 x01| < 2^-29,
+  // where both forms give -1.0f
+  const float xc = 2.0f * x01 - 1.0f;
   const float yp = clenshaw6(xc, 881.979476556478289f, 1496.058452015812463f,
                              908.662212739659481f, 373.566100223287378f, 85.840860336314364f,
                              6.683258861509244f);
@@ -279,11 +293,15 @@ __device__ __forceinline__ void opsin_pixel(const float blurred[3], const float 
 // MaskHighIntensityChangeOpt mixing for one pixel, :739-778.
 // sqr_max_diff is the max over valid 4-neighbours of
 // float(0.5*(c0y[n]+c1y[n]) - ave_y)^2, or -1 when none.
-__device__ __forceinline__ float mhic_ave(float a, float b) {
-  return static_cast<float>((static_cast<double>(a + b)) * 0.5);
-}
+// The reference promotes these to double; in float they are bit-identical:
+// (a + b) * 0.5 is one rounding of the exact half in both, and h - ave with
+// h = 0.5 * (n0 + n1) (exact: the Y sums here are far from subnormal) is the
+// correctly rounded exact difference either way (exact in double when the
+// exponents are within 29 bits of each other; otherwise both round to the
+// larger operand).
+__device__ __forceinline__ float mhic_ave(float a, float b) { return (a + b) * 0.5f; }
 __device__ __forceinline__ float mhic_sqdiff(float n0, float n1, float ave_y) {
-  float d = static_cast<float>(0.5 * static_cast<double>(n0 + n1) - static_cast<double>(ave_y));
+  const float d = (n0 + n1) * 0.5f - ave_y;
   return d * d;
 }
 __device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], const float ave[3],

@@ -10,6 +10,7 @@ rc=$?
 tail -5 gpurun_out/iter_tests.log
 [ $rc -ne 0 ] && exit $rc
 for sz in ${GZ_ITER_SIZES:-1920x1080x95 3840x2160x90}; do
+  [ "$sz" = none ] && continue
   IFS=x read -r W H Q <<< "$sz"
   timeout -k 10 300 python tools/stage_times.py --width $W --height $H --quality $Q \
     > gpurun_out/iter_stages_${W}x${H}.txt 2>&1 || exit $?
@@ -22,4 +23,12 @@ if [ -n "${GZ_ITER_PMC:-}" ]; then
     -d gpurun_out/iter_pmc -o run --output-format csv -- python tools/compare_loop.py --width 3840 --height 2160 --compares 2 \
     > gpurun_out/iter_pmc.json 2> gpurun_out/iter_pmc.err || exit $?
   python tools/pmc_summary.py gpurun_out/iter_pmc > gpurun_out/iter_pmc.txt && cat gpurun_out/iter_pmc.txt
+fi
+if [ -n "${GZ_ITER_PMC2:-}" ]; then
+  export TMPDIR=/tmp
+  rm -rf gpurun_out/iter_pmc2
+  timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_VMEM SQ_WAVE_CYCLES TA_TA_BUSY_sum GRBM_GUI_ACTIVE \
+    -d gpurun_out/iter_pmc2 -o run --output-format csv -- python tools/compare_loop.py --width 3840 --height 2160 --compares 2 \
+    > gpurun_out/iter_pmc2.json 2> gpurun_out/iter_pmc2.err || exit $?
+  python tools/pmc_summary.py gpurun_out/iter_pmc2 > gpurun_out/iter_pmc2.txt && cat gpurun_out/iter_pmc2.txt
 fi
