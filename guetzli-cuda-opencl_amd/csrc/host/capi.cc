@@ -15,6 +15,7 @@
 #include "host/jpeg_encode.h"
 #include "host/jpeg_writer.h"
 #include "host/processor.h"
+#include "host/strips.h"
 #include "host/synthetic.h"
 #include "runtime/engine.h"
 
@@ -258,9 +259,30 @@ gz_status gz_rgb_to_coeffs(const uint8_t* rgb, int width, int height, int16_t* c
   return GZ_OK;
 }
 
+namespace {
+// gz_collectives (C callback) as the host's collective interface.
+class CCollectives : public gz::Collectives {
+ public:
+  explicit CCollectives(const gz_collectives* c) : c_(*c) {}
+  int rank() const override { return c_.rank; }
+  int world() const override { return c_.world; }
+  bool AllGather(const void* send, size_t bytes, void* recv) override {
+    return c_.allgather(c_.ctx, send, bytes, recv) == 0;
+  }
+
+ private:
+  gz_collectives c_;
+};
+
+bool ValidCollectives(const gz_collectives* c) {
+  return c && c->allgather && c->world >= 1 && c->rank >= 0 && c->rank < c->world;
+}
+}  // namespace
+
 static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t* rgb,
                              bool device_ptr, int w, int h, uint8_t** jpeg_out,
-                             size_t* jpeg_size, gz_process_stats* stats) {
+                             size_t* jpeg_size, gz_process_stats* stats,
+                             const gz_collectives* coll = nullptr) {
   if (!params || !rgb || !jpeg_out || !jpeg_size || w <= 0 || h <= 0)
     return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
   if (params->try_420 || params->force_420)
@@ -272,7 +294,13 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
   pp.new_zeroing_model = params->new_zeroing_model != 0;
   gz::ProcessResult res;
   std::string err;
-  const int rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
+  int rc;
+  if (coll) {
+    CCollectives cc(coll);
+    rc = gz::ProcessStrips(device, pp, rgb, w, h, &cc, &res, &err);
+  } else {
+    rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
+  }
   if (rc != 0) return SetError(rc, "process: " + err);
   uint8_t* buf = static_cast<uint8_t*>(std::malloc(res.jpeg.size() ? res.jpeg.size() : 1));
   if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "process: out of host memory");
@@ -314,6 +342,47 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
                                 int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
                                 gz_process_stats* stats) {
   return ProcessImpl(device, params, rgb_dev, true, width, height, jpeg_out, jpeg_size, stats);
+}
+
+gz_status gz_process_rgb_strips(int device, const gz_params* params, const uint8_t* rgb, int width,
+                                int height, const gz_collectives* coll, uint8_t** jpeg_out,
+                                size_t* jpeg_size, gz_process_stats* stats) {
+  if (!ValidCollectives(coll)) return SetError(GZ_ERR_INVALID_ARG, "process_strips: bad collectives");
+  return ProcessImpl(device, params, rgb, false, width, height, jpeg_out, jpeg_size, stats, coll);
+}
+
+gz_status gz_strip_layout(int width, int height, int world, int rank, int* y0, int* y1, int* e0,
+                          int* e1) {
+  if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || !y0 || !y1 || !e0 ||
+      !e1)
+    return SetError(GZ_ERR_INVALID_ARG, "strip_layout: bad argument");
+  const gz::StripLayout L = gz::StripLayout::Make(width, height, world);
+  *y0 = L.y0[rank];
+  *y1 = L.y1[rank];
+  *e0 = L.e0[rank];
+  *e1 = L.e1[rank];
+  return GZ_OK;
+}
+
+gz_status gz_collectives_selftest(const gz_collectives* coll) {
+  if (!ValidCollectives(coll)) return SetError(GZ_ERR_INVALID_ARG, "collectives: bad argument");
+  CCollectives cc(coll);
+  // equal-size gather of a rank-tagged pattern, then a variable-size one
+  const int n = cc.world(), r = cc.rank();
+  std::vector<uint32_t> mine(5), all(5 * n);
+  for (int i = 0; i < 5; ++i) mine[i] = 1000u * r + i;
+  if (!cc.AllGather(mine.data(), mine.size() * 4, all.data()))
+    return SetError(GZ_ERR_INTERNAL, "collectives: all-gather failed");
+  for (int q = 0; q < n; ++q)
+    for (int i = 0; i < 5; ++i)
+      if (all[5 * q + i] != 1000u * q + i) return SetError(GZ_ERR_INTERNAL, "collectives: wrong data");
+  std::vector<uint8_t> v(3 * r + 1, static_cast<uint8_t>(r + 7));
+  std::vector<std::vector<uint8_t>> got;
+  if (!cc.AllGatherV(v, &got)) return SetError(GZ_ERR_INTERNAL, "collectives: all-gather-v failed");
+  for (int q = 0; q < n; ++q)
+    if (got[q] != std::vector<uint8_t>(3 * q + 1, static_cast<uint8_t>(q + 7)))
+      return SetError(GZ_ERR_INTERNAL, "collectives: wrong variable-size data");
+  return GZ_OK;
 }
 
 }  // extern "C"

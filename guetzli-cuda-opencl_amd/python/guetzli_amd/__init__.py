@@ -79,6 +79,16 @@ EXPORTED_SYMBOLS = (
 _lib = None
 
 
+# int allgather(void* ctx, const void* send, size_t bytes, void* recv)
+_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                              ctypes.c_void_p)
+
+
+class _Collectives(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("rank", ctypes.c_int), ("world", ctypes.c_int),
+                ("allgather", _ALLGATHER)]
+
+
 def lib():
     """Load libguetzli_hip.so (raises GuetzliError if it was not built)."""
     global _lib
@@ -130,6 +140,11 @@ def lib():
     L.gz_synthetic_frame.restype = i32
     L.gz_rgb_to_coeffs.argtypes = [vp, i32, i32, vp]
     L.gz_rgb_to_coeffs.restype = i32
+    L.gz_process_rgb_strips.argtypes = [i32, ctypes.POINTER(_Params), vp, i32, i32,
+                                        ctypes.POINTER(_Collectives), ctypes.POINTER(vp),
+                                        ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_Stats)]
+    L.gz_strip_layout.argtypes = [i32, i32, i32, i32] + [ctypes.POINTER(i32)] * 4
+    L.gz_collectives_selftest.argtypes = [ctypes.POINTER(_Collectives)]
     L.gz_profile_enable.argtypes = [i32]
     L.gz_profile_get.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long),
                                  ctypes.POINTER(ctypes.c_double)]
@@ -290,6 +305,89 @@ def process_device(rgb_dev_ptr, width, height, params=None, device=0, return_sta
     _check(L.gz_process_rgb_device(device, ctypes.byref(p), ctypes.c_void_p(rgb_dev_ptr), width,
                                    height, ctypes.byref(out), ctypes.byref(size),
                                    ctypes.byref(st)), "process_device")
+    data = ctypes.string_at(out, size.value)
+    L.gz_free(out)
+    if return_stats:
+        return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
+                                  st.compares, st.seconds_compare, st.seconds_zeroing,
+                                  st.seconds_total, st.seconds_setup, st.seconds_write,
+                                  st.seconds_quantize, st.seconds_backend)
+    return data
+
+
+class Collectives:
+    """The exchange of a multi-rank encode (gz_collectives): an equal-size
+    all-gather of byte blocks.  `allgather(data: bytes) -> bytes` must return
+    every rank's block concatenated in rank order.  Keeps the ctypes callback
+    alive for as long as the object lives."""
+
+    def __init__(self, rank, world, allgather):
+        self.rank, self.world = rank, world
+        self._fn = allgather
+
+        def cb(_ctx, send, nbytes, recv):
+            try:
+                data = ctypes.string_at(send, nbytes) if nbytes else b""
+                out = self._fn(data)
+                if len(out) != nbytes * self.world:
+                    return 1
+                if out:
+                    ctypes.memmove(recv, out, len(out))
+                return 0
+            except Exception:  # an exception cannot cross the C boundary
+                return 1
+
+        self._cb = _ALLGATHER(cb)
+        self._c = _Collectives(None, rank, world, self._cb)
+
+    @classmethod
+    def from_torch(cls, dist, device="cpu"):
+        """Bound to torch.distributed: all_gather_into_tensor of uint8 blocks on
+        `device` ("cuda:N" for RCCL over xGMI with the nccl backend, "cpu" for
+        gloo)."""
+        import torch
+
+        world, rank = dist.get_world_size(), dist.get_rank()
+
+        def allgather(data):
+            n = len(data)
+            src = torch.zeros(max(n, 1), dtype=torch.uint8)
+            if n:
+                src[:n] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            src = src.to(device)
+            dst = torch.empty(world * src.numel(), dtype=torch.uint8, device=device)
+            dist.all_gather_into_tensor(dst, src)
+            blocks = dst.view(world, -1)[:, :n].cpu().numpy()
+            return blocks.tobytes()
+
+        return cls(rank, world, allgather)
+
+    def selftest(self):
+        _check(lib().gz_collectives_selftest(ctypes.byref(self._c)), "collectives_selftest")
+
+
+def strip_layout(width, height, world, rank):
+    """(y0, y1, e0, e1): rows rank `rank` owns and computes when one frame is
+    split over `world` GPUs."""
+    v = [ctypes.c_int() for _ in range(4)]
+    _check(lib().gz_strip_layout(width, height, world, rank, *[ctypes.byref(x) for x in v]),
+           "strip_layout")
+    return tuple(x.value for x in v)
+
+
+def process_strips(rgb, width, height, collectives, params=None, device=0, return_stats=False):
+    """guetzli::Process of one frame split over the ranks of `collectives`
+    (row strips + halo, one GPU per rank); every rank passes the whole frame
+    and gets the same bytes as process()."""
+    L = lib()
+    a = _as_rgb(rgb, width, height)
+    p = (params or Params())._c()
+    out = ctypes.c_void_p()
+    size = ctypes.c_size_t()
+    st = _Stats()
+    _check(L.gz_process_rgb_strips(device, ctypes.byref(p), _ptr(a), width, height,
+                                   ctypes.byref(collectives._c), ctypes.byref(out),
+                                   ctypes.byref(size), ctypes.byref(st)), "process_strips")
     data = ctypes.string_at(out, size.value)
     L.gz_free(out)
     if return_stats:

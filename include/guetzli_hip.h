@@ -114,6 +114,30 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
                                 int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
                                 gz_process_stats* stats);
 
+/* ---- one frame over several GPUs (row strips + halo) ------------------ */
+/* The exchange a multi-rank encode needs: an equal-size all-gather (every
+ * rank contributes `bytes` bytes, `recv` receives world*bytes in rank order);
+ * returns 0 on success.  Bound to torch.distributed (RCCL over xGMI, or gloo)
+ * by the Python package. */
+typedef struct {
+  void* ctx;
+  int rank;
+  int world;
+  int (*allgather)(void* ctx, const void* send, size_t bytes, void* recv);
+} gz_collectives;
+/* guetzli::Process (processor.h:62-64) for one frame whose Butteraugli passes
+ * are split over the ranks of `coll` by rows: every rank passes the whole
+ * RGB frame (host memory) and its own device, and receives the same bytes as
+ * gz_process_rgb.  A rank computes its owned rows plus a 96-row halo. */
+gz_status gz_process_rgb_strips(int device, const gz_params* params, const uint8_t* rgb, int width,
+                                int height, const gz_collectives* coll, uint8_t** jpeg_out,
+                                size_t* jpeg_size, gz_process_stats* stats);
+/* Rows rank `rank` owns [y0, y1) and computes [e0, e1). */
+gz_status gz_strip_layout(int width, int height, int world, int rank, int* y0, int* y1, int* e0,
+                          int* e1);
+/* Exercises `coll` (fixed- and variable-size gathers); GZ_OK if consistent. */
+gz_status gz_collectives_selftest(const gz_collectives* coll);
+
 /* ---- comparator (guetzli::ButteraugliComparator) ---------------------- */
 /* ButteraugliComparator(w, h, rgb, target, stats) ctor
  * (guetzli/butteraugli_comparator.cc:48-58); width, height >= 8. */

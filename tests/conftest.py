@@ -47,11 +47,13 @@ def _native_bin(name, with_oracle):
     lib_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "lib")
     oracle_dir = os.path.join(ROOT, "oracle", "_build")
     host_dir = os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc", "host")
+    native_dir = os.path.join(ROOT, "tests", "native")
     deps = [src, os.path.join(lib_dir, "libguetzli_hip.so")] + [
+        os.path.join(native_dir, f) for f in os.listdir(native_dir) if f.endswith(".h")] + [
         os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith(".h")]
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
-        cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+        cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread",
                "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
                "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
                src, "-o", out, "-L", lib_dir, "-lguetzli_hip", "-Wl,-rpath," + lib_dir]
@@ -59,6 +61,12 @@ def _native_bin(name, with_oracle):
             cmd += ["-L", oracle_dir, "-lgz_oracle", "-Wl,-rpath," + oracle_dir]
         subprocess.run(cmd, check=True)
     return out
+
+
+@pytest.fixture(scope="session")
+def strips_e2e_bin():
+    """tests/native/strips_oracle_e2e: row strips over threads, oracle comparators."""
+    return _native_bin("strips_oracle_e2e", True)
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,120 @@
+// CPU end-to-end check of the row-strip decomposition (host/strips.h): WORLD
+// ranks run as threads, each with the product's StripComparator over a
+// CPU-oracle comparator of its strip (rows + halo) and an in-process
+// all-gather; every rank must produce the single-comparator bytes.  Test
+// infrastructure only.
+//
+//   strips_oracle_e2e RGB W H QUALITY WORLD OUT.jpg
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host/strips.h"
+#include "oracle_comparator.h"
+
+namespace {
+
+// Equal-size all-gather among threads: the last rank to arrive publishes
+// the concatenation of the generation's blocks.
+struct Exchange {
+  explicit Exchange(int world) : world(world), slots(world) {}
+  int world;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::vector<uint8_t>> slots;
+  std::vector<uint8_t> result;
+  int arrived = 0;
+  unsigned long gen = 0;
+};
+
+class ThreadCollectives : public gz::Collectives {
+ public:
+  ThreadCollectives(Exchange* x, int rank) : x_(x), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int world() const override { return x_->world; }
+  bool AllGather(const void* send, size_t bytes, void* recv) override {
+    std::unique_lock<std::mutex> lk(x_->mu);
+    const auto* p = static_cast<const uint8_t*>(send);
+    x_->slots[rank_].assign(p, p + bytes);
+    const unsigned long g = x_->gen;
+    if (++x_->arrived == x_->world) {
+      x_->result.clear();
+      for (auto& s : x_->slots) {
+        if (s.size() != bytes) return false;
+        x_->result.insert(x_->result.end(), s.begin(), s.end());
+      }
+      x_->arrived = 0;
+      ++x_->gen;
+      x_->cv.notify_all();
+    } else {
+      x_->cv.wait(lk, [&] { return x_->gen != g; });
+    }
+    std::memcpy(recv, x_->result.data(), bytes * x_->world);
+    return true;
+  }
+
+ private:
+  Exchange* x_;
+  int rank_;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 7) {
+    fprintf(stderr, "usage: strips_oracle_e2e RGB W H QUALITY WORLD OUT.jpg\n");
+    return 1;
+  }
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  const int w = atoi(argv[2]), h = atoi(argv[3]), q = atoi(argv[4]), world = atoi(argv[5]);
+  std::vector<uint8_t> rgb(3 * static_cast<size_t>(w) * h);
+  if (fread(rgb.data(), 1, rgb.size(), f) != rgb.size()) return 2;
+  fclose(f);
+  gz::ProcessParams params;
+  params.butteraugli_target = static_cast<float>(gz::ButteraugliScoreForQuality(q));
+  const gz::StripLayout L = gz::StripLayout::Make(w, h, world);
+  Exchange x(world);
+  std::vector<std::string> out(world), errs(world);
+  std::vector<int> rc(world, -1), iters(world, 0);
+  std::vector<std::thread> ranks;
+  for (int r = 0; r < world; ++r) {
+    ranks.emplace_back([&, r] {
+      ThreadCollectives coll(&x, r);
+      gz::JpegData jpg;
+      gz::EncodeRGBToJpegData(rgb.data(), w, h, &jpg);
+      std::unique_ptr<gz::Comparator> inner;
+      if (L.y1[r] > L.y0[r])
+        inner.reset(new gz_test::OracleComparator(w, L.e1[r] - L.e0[r],
+                                                  rgb.data() + static_cast<size_t>(3) * w * L.e0[r],
+                                                  params.butteraugli_target));
+      gz::StripComparator cmp(L, std::move(inner), &coll, params.butteraugli_target);
+      gz::ProcessResult res;
+      rc[r] = gz::ProcessJpegData(params, jpg, &cmp, &res, &errs[r]);
+      out[r] = res.jpeg;
+      iters[r] = res.iterations;
+    });
+  }
+  for (auto& t : ranks) t.join();
+  for (int r = 0; r < world; ++r) {
+    if (rc[r] != 0) {
+      fprintf(stderr, "rank %d failed: %d %s\n", r, rc[r], errs[r].c_str());
+      return 3;
+    }
+    if (out[r] != out[0]) {
+      fprintf(stderr, "rank %d bytes differ from rank 0\n", r);
+      return 4;
+    }
+  }
+  FILE* o = fopen(argv[6], "wb");
+  fwrite(out[0].data(), 1, out[0].size(), o);
+  fclose(o);
+  printf("{\"bytes\": %zu, \"iters\": %d, \"world\": %d}\n", out[0].size(), iters[0], world);
+  return 0;
+}

@@ -1,0 +1,185 @@
+"""One frame over several GPUs: row strips with a halo (SURVEY.md §8e,
+BASELINE configs[4]).
+
+CPU (no GPU needed):
+  * the layout tiles the image with aligned strips;
+  * the halo claim on the CPU oracle: Butteraugli of a strip (owned rows +
+    96-row halo) reproduces the full-image distance map and activity mask on
+    the owned rows bit for bit;
+  * the product's StripComparator over oracle comparators, ranks as threads,
+    reproduces the reference's JPEG bytes (tests/native/strips_oracle_e2e.cc);
+  * the torch.distributed binding of the collectives (gloo, world size 2).
+GPU: every rank on cuda:0 (gloo exchange) reproduces the reference bytes.
+"""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle_lib import GOLDEN, lib as oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+@pytest.mark.parametrize("w,h,world", [(8192, 8192, 4), (444, 258, 2), (444, 258, 3), (64, 40, 4),
+                                       (3840, 2160, 8), (100, 1000, 7)])
+def test_strip_layout_tiles_the_image(gz, w, h, world):
+    prev = 0
+    for r in range(world):
+        y0, y1, e0, e1 = gz.strip_layout(w, h, world, r)
+        assert y0 == prev and y1 >= y0
+        assert y0 % 24 == 0 or y0 == h
+        if y1 > y0:
+            assert e0 == max(0, y0 - 96) and e1 == min(h, y1 + 96)
+        prev = y1
+    assert prev == h
+
+
+def _quantized_candidate(gz, rgb, w, h, seed):
+    coeffs = gz.rgb_to_coeffs(rgb, w, h)
+    rng = np.random.default_rng(seed)
+    q = rng.integers(1, 14, size=(3, 64))
+    nb = ((w + 7) // 8) * ((h + 7) // 8)
+    c = coeffs.reshape(3, nb, 64).astype(np.int32)
+    qq = q[:, None, :]
+    r = np.fmod(c, qq)
+    return (c + np.where(2 * r > qq, qq - r, np.where(-2 * r > qq, -qq - r, -r))).astype(np.int16)
+
+
+@pytest.mark.parametrize("w,h,world,seed", [(72, 456, 3, 1), (40, 300, 2, 2)])
+def test_oracle_strip_equals_full_image_on_owned_rows(gz, w, h, world, seed):
+    """The halo claim of host/strips.h on the CPU oracle: distance map and
+    (reference) activity mask of each strip equal the full image's on the
+    rows the strip owns."""
+    L = oracle()
+    rgb = gz.synthetic_frame(seed, w, h)
+    cand = _quantized_candidate(gz, rgb, w, h, seed)
+    bw = (w + 7) // 8
+    full = np.zeros(w * h, np.float32)
+    L.gzo_compare(w, h, rgb.ravel(), cand.ravel(), full)
+    full = full.reshape(h, w)
+
+    def mask_of(img, hh):
+        n = w * hh
+        ref = np.zeros(3 * n, np.float32)
+        L.gzo_srgb_to_linear_planes(w, hh, np.ascontiguousarray(img).ravel(), ref)
+        L.gzo_opsin_dynamics(w, hh, ref)
+        m = np.zeros(3 * n, np.float32)
+        dc = np.zeros(3 * n, np.float32)
+        L.gzo_mask(w, hh, ref, ref, m, dc)
+        return m.reshape(3, hh, w), dc.reshape(3, hh, w)
+
+    full_mask, full_dc = mask_of(rgb, h)
+    for r in range(world):
+        y0, y1, e0, e1 = gz.strip_layout(w, h, world, r)
+        if y1 == y0:
+            continue
+        hs = e1 - e0
+        sub_rgb = np.ascontiguousarray(rgb[e0:e1])
+        sub = np.ascontiguousarray(cand[:, (e0 // 8) * bw:((e1 + 7) // 8) * bw, :])
+        dm = np.zeros(w * hs, np.float32)
+        L.gzo_compare(w, hs, sub_rgb.ravel(), sub.ravel(), dm)
+        dm = dm.reshape(hs, w)
+        got, want = dm[y0 - e0:y1 - e0], full[y0:y1]
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+            "rank %d: %d distance values differ" % (r, int((got != want).sum()))
+        m, dc = mask_of(sub_rgb, hs)
+        assert np.array_equal(m[:, y0 - e0:y1 - e0], full_mask[:, y0:y1])
+        assert np.array_equal(dc[:, y0 - e0:y1 - e0], full_dc[:, y0:y1])
+
+
+@pytest.mark.parametrize("name,world", [("bees_q95", 2), ("bees_q84", 3)])
+def test_strip_comparator_threads_reproduce_reference(strips_e2e_bin, name, world, tmp_path):
+    """StripComparator (product host code) with oracle strip comparators:
+    every rank's bytes equal the reference `guetzli --c` known answer."""
+    e = MANIFEST["e2e"][name]
+    out = tmp_path / "out.jpg"
+    res = subprocess.run([strips_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]),
+                          str(e["h"]), str(e["quality"]), str(world), str(out)],
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr
+    info = json.loads(res.stdout)
+    assert info["iters"] == e["iters"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _gloo_selftest(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+    import torch.distributed as dist
+    import guetzli_amd as gz
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    try:
+        c = gz.Collectives.from_torch(dist, "cpu")
+        c.selftest()
+        q.put((rank, "ok"))
+    except Exception as ex:  # reported to the parent
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_torch_collectives_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_selftest, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: "ok", 1: "ok"}
+
+
+def _gpu_strip_rank(rank, world, port, e, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+    import torch.distributed as dist
+    import guetzli_amd as gz
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    try:
+        rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+        coll = gz.Collectives.from_torch(dist, "cpu")
+        data = gz.process_strips(rgb, e["w"], e["h"], coll, gz.Params.for_quality(e["quality"]),
+                                 device=0)
+        q.put((rank, hashlib.sha256(data).hexdigest()))
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", [("bees_q95", 1), ("bees_q90", 2)])
+def test_gpu_strips_reproduce_reference(name, world):
+    """`world` ranks, each a process with its strip's engine on cuda:0, the
+    exchange over gloo: every rank returns the reference bytes."""
+    import torch.multiprocessing as mp
+    e = MANIFEST["e2e"][name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_strip_rank, args=(r, world, port, e, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert all(v == e["sha256"] for v in res.values()), res
