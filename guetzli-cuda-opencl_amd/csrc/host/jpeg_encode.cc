@@ -4,6 +4,7 @@
 // reciprocal-multiply quantizer.  All arithmetic is 32-bit integer with the
 // reference's truncations to int16 at every store.
 #include "host/jpeg_encode.h"
+#include "host/thread_pool.h"
 
 #include <algorithm>
 #include <cstring>
@@ -92,7 +93,8 @@ void RgbToCoeffsQ1(const uint8_t* rgb, int w, int h, int16_t* coeffs) {
   const size_t nb = static_cast<size_t>(bw) * bh;
   // quantizer at q = 1: iquant = ((1 << 16) + 1) / 1, bias 0x80 << 12, shift 20
   const uint32_t kIQuant = 65537u, kBias = 0x80u << 12;
-  for (int by = 0; by < bh; ++by) {
+  // block rows are independent: spread them over the host pool
+  ParallelFor(bh, [&](int by) {
     for (int bx = 0; bx < bw; ++bx) {
       int16_t blk[3][64];
       for (int iy = 0; iy < 8; ++iy) {
@@ -115,7 +117,7 @@ void RgbToCoeffsQ1(const uint8_t* rgb, int w, int h, int16_t* coeffs) {
         }
       }
     }
-  }
+  });
 }
 
 }  // namespace gz
