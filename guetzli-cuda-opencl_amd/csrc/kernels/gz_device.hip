@@ -136,6 +136,8 @@ void BuildTables(GzTables* t) {
   BuildBlur(14.2644604355f, 0.0f, &t->blur[kSigMaskY]);
   BuildBlur(4.53358927369f, 0.0f, &t->blur[kSigMaskB]);
   BuildBlur(8.8510880283f, 0.03027655136f, &t->blur[kSigDiffmap]);
+  t->blur[kSigMaskBSub] = t->blur[kSigMaskB];
+  t->blur[kSigMaskBSub].step = 3;
   // blur_scale() of the sigma-1.1 blur at each position of an 8-pixel axis
   // (the 8x8-local opsin of SwitchBlock / CompareBlock); same float sum and
   // double normalisation as the device function
@@ -191,8 +193,18 @@ inline int VColSegments(int sig, int h) {
     case kSigMaskX: return vcol_segments<kSigMaskX>(h);
     case kSigMaskY: return vcol_segments<kSigMaskY>(h);
     case kSigMaskB: return vcol_segments<kSigMaskB>(h);
+    case kSigMaskBSub: return vcol_segments<kSigMaskBSub>(h);
     default: return vcol_segments<kSigDiffmap>(h);
   }
+}
+// The blurred mask planes (in down-sampled form) at base + c * n.
+inline MaskPlanes MaskPlanesOf(const float* base, size_t n, bool sub_b) {
+  MaskPlanes mk{};
+  for (int c = 0; c < 3; ++c) {
+    mk.p[c] = base + c * n;
+    mk.step[c] = HostTables().blur[c == 2 && sub_b ? kSigMaskBSub : kSigMaskX + c].step;
+  }
+  return mk;
 }
 inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
   bp.nplanes = planes;
@@ -584,7 +596,7 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   return true;
 }
 
-bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
+bool Engine::MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   {
     const int strips = (w_ + kMsCols - 1) / kMsCols, segs = (h_ + kMsRows - 1) / kMsRows;
@@ -596,7 +608,7 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1) {
   for (int c = 0; c < 3; ++c) {
     bp.in[c] = d_mb_ + c * n_;
     bp.out[c] = d_tmp_ + c * n_;
-    bp.sig[c] = kSigMaskX + c;
+    bp.sig[c] = c == 2 && sub_b ? kSigMaskBSub : kSigMaskX + c;
   }
   const dim3 grid2 = BlurH4Grid(w_, h_, 3, bp);  // fills bp's packed-grid fields
   GZ_TIMED("mask_blur_h", k_blur_h4<kBlurMask><<<grid2, 256, 0, s>>>(
@@ -690,8 +702,11 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
   // S9-S13: activity mask
-  if (!MaskPipeline(d_m0_, d_m1_)) return false;
-  MaskPlanes mk{{d_ma_, d_ma_ + n, d_ma_ + 2 * n}};
+  // the full B mask only for the stage dumps; Compare itself samples it at
+  // (3j + 3, 3i + 3) alone
+  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc);
+  if (!MaskPipeline(d_m0_, d_m1_, !full_mask)) return false;
+  MaskPlanes mk = MaskPlanesOf(d_ma_, n, !full_mask);
   if (dbg && (dbg->mask || dbg->mask_dc)) {
     GZ_TIMED("mask_full_dbg", k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_));
     if (!d2h(dbg->mask, d_mb_, 3 * n)) return false;
@@ -765,8 +780,8 @@ bool Engine::StartBlockComparisons(float* mask_scale_host) {
   GZ_HIP(hipSetDevice(device_));
   // ButteraugliComparator::StartBlockComparisons: Mask(rgb0, rgb0) with no
   // high-intensity masking (butteraugli_comparator.cc:72-79).
-  if (!MaskPipeline(d_ref_xyb_, d_ref_xyb_)) return false;
-  MaskPlanes mk{{d_ma_, d_ma_ + n_, d_ma_ + 2 * n_}};
+  if (!MaskPipeline(d_ref_xyb_, d_ref_xyb_, false)) return false;
+  MaskPlanes mk = MaskPlanesOf(d_ma_, n_, false);
   GZ_TIMED("mask_scale", k_mask_scale<<<(nb_ + 255) / 256, 256, 0, s>>>(mk, w_, h_, bw_, nb_, d_mask_scale_));
   if (mask_scale_host)
     GZ_HIP(hipMemcpyAsync(mask_scale_host, d_mask_scale_, 3 * nb_ * 4, hipMemcpyDeviceToHost, s));

@@ -15,7 +15,7 @@
 namespace gz {
 
 constexpr int kMaxTaps = 72;   // largest blur: sigma 14.26 -> 65 taps
-constexpr int kNumSigmas = 9;
+constexpr int kNumSigmas = 10;
 
 // Blur kernels used by the path (clbutter_comparator.cpp:57-94 callers).
 enum SigmaId : int {
@@ -28,6 +28,11 @@ enum SigmaId : int {
   kSigMaskY = 6,   // 14.2644604355
   kSigMaskB = 7,   // 4.53358927369
   kSigDiffmap = 8, // 8.8510880283 (border_ratio 0.03027655136) CalculateDiffmapOpt :958
+  // kSigMaskB evaluated on every 3rd row and column only: per Compare the B
+  // activity mask is read at (3j + 3, 3i + 3) alone (CombineChannelsOpt
+  // :1542-1565), so its blur is run as a step-3 blur with the sigma-4.53
+  // taps -- the same sums at the sampled positions, a ninth of the outputs
+  kSigMaskBSub = 9,
 };
 
 // Compile-time geometry of the nine blurs (BlurOpt, clbutter_comparator.cpp:
@@ -49,8 +54,9 @@ template <> struct BlurGeom<kSigMaskX> { static constexpr int R = 21, STEP = 3; 
 template <> struct BlurGeom<kSigMaskY> { static constexpr int R = 32, STEP = 4; };
 template <> struct BlurGeom<kSigMaskB> { static constexpr int R = 10, STEP = 1; };
 template <> struct BlurGeom<kSigDiffmap> { static constexpr int R = 19, STEP = 2; };
-constexpr int kBlurGeomR[9] = {2, 3, 1, 1, 31, 21, 32, 10, 19};
-constexpr int kBlurGeomStep[9] = {1, 1, 1, 1, 4, 3, 4, 1, 2};
+template <> struct BlurGeom<kSigMaskBSub> { static constexpr int R = 10, STEP = 3; };
+constexpr int kBlurGeomR[kNumSigmas] = {2, 3, 1, 1, 31, 21, 32, 10, 19, 10};
+constexpr int kBlurGeomStep[kNumSigmas] = {1, 1, 1, 1, 4, 3, 4, 1, 2, 3};
 
 // Calls F(kSig) for the (uniform) runtime sigma id.
 #define GZ_BLUR_SWITCH(sig, F)            \
@@ -63,6 +69,7 @@ constexpr int kBlurGeomStep[9] = {1, 1, 1, 1, 4, 3, 4, 1, 2};
     case kSigMaskX: F(kSigMaskX); break;  \
     case kSigMaskY: F(kSigMaskY); break;  \
     case kSigMaskB: F(kSigMaskB); break;  \
+    case kSigMaskBSub: F(kSigMaskBSub); break; \
     default: F(kSigDiffmap); break;       \
   }
 

@@ -122,7 +122,7 @@ class Engine {
     void* stop;
   };
   std::vector<PendingEvent> pending_;
-  bool MaskPipeline(const float* xyb0, const float* xyb1);
+  bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b);
   bool EnqueueCompare(CompareDebug* dbg);
   void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
 

@@ -173,3 +173,31 @@ def test_compare_matches_oracle_on_synthetic(gz, w, h, seed):
     d = L.gzo_compare(w, h, rgb.ravel(), cand, dm)
     assert bits_equal(st["distmap"], dm), mismatch(st["distmap"], dm)
     assert np.float32(st["distance"]) == np.float32(d)
+
+
+@pytest.mark.parametrize("w,h,seed", [(256, 256, 7), (333, 197, 8), (517, 389, 4)])
+def test_compare_fast_path_matches_oracle(gz, w, h, seed):
+    """The Compare pass as the search runs it (graph-launched, no stage dumps,
+    the B activity mask evaluated only where CombineChannels samples it):
+    distance and per-block maxima equal the CPU oracle's."""
+    L = oracle()
+    rgb = gz.synthetic_frame(seed, w, h)
+    coeffs = gz.rgb_to_coeffs(rgb, w, h)
+    rng = np.random.default_rng(seed)
+    q = rng.integers(1, 12, size=(3, 64))
+    nb = ((w + 7) // 8) * ((h + 7) // 8)
+    c = coeffs.reshape(3, nb, 64).astype(np.int32)
+    qq = q[:, None, :]
+    r = np.fmod(c, qq)
+    cand = (c + np.where(2 * r > qq, qq - r, np.where(-2 * r > qq, -qq - r, -r))).astype(np.int16).ravel()
+    cmp = gz.ButteraugliComparator(w, h, rgb, 1.0)
+    d = cmp.compare(cand)
+    d2 = cmp.compare(cand)  # graph replay
+    dm = np.zeros(w * h, np.float32)
+    dref = L.gzo_compare(w, h, rgb.ravel(), cand, dm)
+    assert np.float32(d) == np.float32(dref) and np.float32(d2) == np.float32(dref)
+    bw, bh = (w + 7) // 8, (h + 7) // 8
+    dm = dm.reshape(h, w)
+    bm = np.array([max(0.0, dm[8 * by:8 * by + 8, 8 * bx:8 * bx + 8].max())
+                   for by in range(bh) for bx in range(bw)], np.float32)
+    assert bits_equal(cmp.block_max(), bm)
