@@ -206,6 +206,18 @@ inline MaskPlanes MaskPlanesOf(const float* base, size_t n, bool sub_b) {
   }
   return mk;
 }
+// Workgroups of k_blur_vlds: per plane (64-column group, kVlOut-row segment).
+inline dim3 BlurVLdsGrid(int w, int h, int planes, BlurPlanes& bp) {
+  bp.nplanes = planes;
+  bp.start[0] = 0;
+  for (int p = 0; p < planes; ++p) {
+    const int st = HostTables().blur[bp.sig[p]].step;
+    const int dx = (w + st - 1) / st, dy = (h + st - 1) / st;
+    bp.tiles[p] = (dx + 63) / 64;
+    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * ((dy + kVlOut - 1) / kVlOut);
+  }
+  return dim3(bp.start[planes]);
+}
 inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
   bp.nplanes = planes;
   bp.start[0] = 0;
@@ -217,14 +229,25 @@ inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
   }
   return dim3((bp.start[planes] + 3) / 4);
 }
-// Wave items of k_blur_h4: per plane (256-output band, row).
+// Outputs of one k_blur_h4 wave for a sigma.
+inline int H4Outputs(int sig) {
+  switch (sig) {
+    case kSigLowFreq: return H4Geom<kSigLowFreq, H4K<kSigLowFreq>::K>::OUT;
+    case kSigMaskX: return H4Geom<kSigMaskX, H4K<kSigMaskX>::K>::OUT;
+    case kSigMaskY: return H4Geom<kSigMaskY, H4K<kSigMaskY>::K>::OUT;
+    case kSigMaskB: return H4Geom<kSigMaskB, H4K<kSigMaskB>::K>::OUT;
+    case kSigMaskBSub: return H4Geom<kSigMaskBSub, H4K<kSigMaskBSub>::K>::OUT;
+    default: return H4Geom<kSigDiffmap, H4K<kSigDiffmap>::K>::OUT;
+  }
+}
+// Wave items of k_blur_h4: per plane (band of H4Outputs, row).
 inline dim3 BlurH4Grid(int w, int h, int planes, BlurPlanes& bp) {
   bp.nplanes = planes;
   bp.start[0] = 0;
   for (int p = 0; p < planes; ++p) {
     const int st = HostTables().blur[bp.sig[p]].step;
     const int dx = (w + st - 1) / st;
-    bp.tiles[p] = (dx + 255) / 256;
+    bp.tiles[p] = (dx + H4Outputs(bp.sig[p]) - 1) / H4Outputs(bp.sig[p]);
     bp.start[p + 1] = bp.start[p] + bp.tiles[p] * h;
   }
   return dim3((bp.start[planes] + 3) / 4);
@@ -617,8 +640,8 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  const dim3 grid3 = BlurVColGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("mask_blur_v", k_blur_vcol<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  const dim3 grid3 = BlurVLdsGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_v", k_blur_vlds<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -696,8 +719,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    const dim3 grid8 = BlurVColGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-    GZ_TIMED("lowfreq_blur_v", k_blur_vcol<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    const dim3 grid8 = BlurVLdsGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("lowfreq_blur_v", k_blur_vlds<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -729,8 +752,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
         RowsDiffmap{d_resval_, rw_}, bd, wc, hc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    const dim3 grid10 = BlurVColGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_v", k_blur_vcol<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
+    const dim3 grid10 = BlurVLdsGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_v", k_blur_vlds<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
