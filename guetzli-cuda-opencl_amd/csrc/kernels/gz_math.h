@@ -135,6 +135,11 @@ __device__ __forceinline__ BlockId xcd_block_id() {
 // Small helpers
 // ---------------------------------------------------------------------------
 
+// Index of this thread's wave in a 256-thread workgroup, as a wave-uniform
+// (scalar) value: lets the compiler keep per-wave work items, loop bounds
+// and branches in SGPRs instead of treating them as lane-divergent.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // Lane shifts by DPP (a VALU modifier, no LDS round trip): wave_next(v) is
 // lane i+1's value in lane i, wave_prev(v) lane i-1's; the edge lane gets 0.
 // Call them with the whole wave active (outside lane-divergent branches).
