@@ -140,6 +140,13 @@ __device__ __forceinline__ BlockId xcd_block_id() {
 // and branches in SGPRs instead of treating them as lane-divergent.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// v where keep, else +0, by a bit mask: loads stay unconditional (a select
+// on a loaded value may otherwise become a branch around the load that
+// waits for it on the spot).
+__device__ __forceinline__ float masked(float v, bool keep) {
+  return __int_as_float(__float_as_int(v) & (keep ? -1 : 0));
+}
+
 // Lane shifts by DPP (a VALU modifier, no LDS round trip): wave_next(v) is
 // lane i+1's value in lane i, wave_prev(v) lane i-1's; the edge lane gets 0.
 // Call them with the whole wave active (outside lane-divergent branches).
