@@ -140,6 +140,14 @@ __device__ __forceinline__ BlockId xcd_block_id() {
 // and branches in SGPRs instead of treating them as lane-divergent.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// Row y of a plane of width w: with y wave-uniform the pointer is formed in
+// scalar registers and a lane's access is a 32-bit offset from it (saddr +
+// voffset addressing: no 64-bit address arithmetic per lane).
+template <class T>
+__device__ __forceinline__ T* row_ptr(T* base, int y, int w) {
+  return base + static_cast<size_t>(y) * w;
+}
+
 // v where keep, else +0, by a bit mask: loads stay unconditional (a select
 // on a loaded value may otherwise become a branch around the load that
 // waits for it on the spot).
