@@ -656,9 +656,14 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     return true;
   };
   ProfBegin("compare_pass");
-  GZ_HIP(hipMemsetAsync(d_edge_, 0, 3 * rn * 4, s));
-  GZ_HIP(hipMemsetAsync(d_dc_, 0, 3 * rn * 4, s));
-  GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
+  // Res points that k_edge_map / k_block_diff skip are never read by
+  // k_combine (it reads only ry + 5 < h, rx + 5 < w, all written this pass),
+  // so the zeroing is only for the stage dumps, which compare whole arrays.
+  if (dbg) {
+    GZ_HIP(hipMemsetAsync(d_edge_, 0, 3 * rn * 4, s));
+    GZ_HIP(hipMemsetAsync(d_dc_, 0, 3 * rn * 4, s));
+    GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
+  }
   // S0: candidate coefficients -> linear RGB
   GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_));
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
