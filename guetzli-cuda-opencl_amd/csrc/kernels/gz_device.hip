@@ -670,10 +670,12 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // S1-S3: opsin dynamics (blur + transform) and high intensity change
   // masking, fused
   {
-    const int strips = (w_ + kOsCols - 1) / kOsCols, segs = (h_ + kOsRows - 1) / kOsRows;
+    const int rows = OpsinStreamRows(w_, h_);
+    const int strips = (w_ + kOsCols - 1) / kOsCols, segs = (h_ + rows - 1) / rows;
     float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
     GZ_TIMED("opsin_mhic", k_opsin_mhic_stream<<<(strips * segs + 3) / 4, 256, 0, s>>>(
-        d_lin_, d_ref_xyb_, w_, h_, strips, segs, d_m0_, d_m1_, xyb_dbg, d_scales_, scale_stride_));
+        d_lin_, d_ref_xyb_, w_, h_, strips, segs, rows, d_m0_, d_m1_, xyb_dbg, d_scales_,
+        scale_stride_));
     if (xyb_dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   }
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
