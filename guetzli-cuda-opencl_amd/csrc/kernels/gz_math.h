@@ -284,6 +284,19 @@ __device__ __forceinline__ float clenshaw6(float x, float c0, float c1, float c2
   return xb - b2 + c0;
 }
 
+__device__ __forceinline__ f32x2 clenshaw6x2(float x, f32x2 c0, f32x2 c1, f32x2 c2, f32x2 c3,
+                                             f32x2 c4, f32x2 c5) {
+  const f32x2 xx = {x, x};
+  f32x2 b1 = {0.0f, 0.0f}, b2 = {0.0f, 0.0f}, xb, t;
+  xb = xx * b1; t = (xb + xb) - b2 + c5; b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + c4; b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + c3; b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + c2; b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + c1; b2 = b1; b1 = t;
+  xb = xx * b1;
+  return xb - b2 + c0;
+}
+
 __device__ __forceinline__ float gamma_poly(float x) {
   // GammaPolynomialOpt, :861-874 (RationalPolynomialOpt :828-859)
   const float lo = 0.770000000000000f, hi = 274.579999999999984f;
@@ -292,12 +305,15 @@ __device__ __forceinline__ float gamma_poly(float x) {
   // exact, and the difference is exact in double unless |2 x01| < 2^-29,
   // where both forms give -1.0f
   const float xc = 2.0f * x01 - 1.0f;
-  const float yp = clenshaw6(xc, 881.979476556478289f, 1496.058452015812463f,
-                             908.662212739659481f, 373.566100223287378f, 85.840860336314364f,
-                             6.683258861509244f);
-  const float yq = clenshaw6(xc, 12.262350348616792f, 20.557285797683576f,
-                             12.161463238367844f, 4.711532733641639f, 0.899112889751053f,
-                             0.035662329617191f);
+  // numerator and denominator recursions side by side in packed f32 (each
+  // half is clenshaw6's exact operation sequence)
+  const f32x2 r = clenshaw6x2(xc, f32x2{881.979476556478289f, 12.262350348616792f},
+                              f32x2{1496.058452015812463f, 20.557285797683576f},
+                              f32x2{908.662212739659481f, 12.161463238367844f},
+                              f32x2{373.566100223287378f, 4.711532733641639f},
+                              f32x2{85.840860336314364f, 0.899112889751053f},
+                              f32x2{6.683258861509244f, 0.035662329617191f});
+  const float yp = r.x, yq = r.y;
   if (yq == 0.0f) return 0.0f;
   return yp / yq;
 }
