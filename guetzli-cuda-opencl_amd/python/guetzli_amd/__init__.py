@@ -73,7 +73,8 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
     "gz_comparator_original_coeffs", "gz_comparator_write_jpeg", "gz_write_jpeg_host",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
-    "gz_last_process_detail",
+    "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
+    "gz_collectives_selftest",
 )
 
 _lib = None
