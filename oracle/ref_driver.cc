@@ -8,6 +8,8 @@
 //
 //   guetzli_ref encode  RGB W H QUALITY OUT.jpg [c|cpu]     guetzli.cc:247-368
 //   guetzli_ref stages  RGB W H QSEED OUTDIR                 see dump_stages()
+//   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg            processor.cc:1029-1066
+//   guetzli_ref decode  IN.jpg OUT.rgb OUT.coeffs             ReadJpeg + DecodeJpegToRGB
 //
 // RGB files are raw interleaved 8-bit (no header).  All dumps are raw
 // little-endian arrays; OUTDIR/meta.txt lists them.
@@ -97,6 +99,50 @@ int Encode(int argc, char** argv) {
   WriteAll(argv[6], out.data(), out.size());
   fprintf(stdout, "{\"bytes\": %zu, \"seconds\": %.6f, \"iters\": %d}\n", out.size(), dt,
           stats.counters[guetzli::kNumItersCnt]);
+  return 0;
+}
+
+// guetzli::Process on a JPEG file (processor.cc:1029-1066), --c mode:
+//   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg
+int EncodeJpeg(int argc, char** argv) {
+  if (argc < 5) return 1;
+  std::vector<uint8_t> in = ReadAll(argv[2]);
+  const int quality = atoi(argv[3]);
+  g_mathMode = MODE_CPU_OPT;
+  guetzli::Params params;
+  params.butteraugli_target =
+      static_cast<float>(guetzli::ButteraugliScoreForQuality(quality));
+  guetzli::ProcessStats stats;
+  std::string out;
+  const std::string data(in.begin(), in.end());
+  auto t0 = std::chrono::steady_clock::now();
+  const bool ok = guetzli::Process(params, &stats, data, &out);
+  double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (!ok) { fprintf(stderr, "Process failed\n"); return 3; }
+  WriteAll(argv[4], out.data(), out.size());
+  fprintf(stdout, "{\"bytes\": %zu, \"seconds\": %.6f, \"iters\": %d}\n", out.size(), dt,
+          stats.counters[guetzli::kNumItersCnt]);
+  return 0;
+}
+
+// ReadJpeg + DecodeJpegToRGB (jpeg_data_reader.cc, jpeg_data_decoder.cc:45-53):
+//   guetzli_ref decode IN.jpg OUT.rgb OUT.coeffs
+// OUT.coeffs: int16 [3][blocks][64] quantized coefficients, natural order.
+int Decode(int argc, char** argv) {
+  if (argc < 5) return 1;
+  std::vector<uint8_t> in = ReadAll(argv[2]);
+  guetzli::JPEGData jpg;
+  if (!guetzli::ReadJpeg(in.data(), in.size(), guetzli::JPEG_READ_ALL, &jpg)) {
+    fprintf(stderr, "ReadJpeg failed\n");
+    return 3;
+  }
+  std::vector<uint8_t> rgb = guetzli::DecodeJpegToRGB(jpg);
+  WriteAll(argv[3], rgb.data(), rgb.size());
+  std::vector<int16_t> co;
+  for (const auto& c : jpg.components) co.insert(co.end(), c.coeffs.begin(), c.coeffs.end());
+  WriteAll(argv[4], co.data(), co.size() * sizeof(int16_t));
+  fprintf(stdout, "{\"w\": %d, \"h\": %d, \"ncomp\": %zu, \"rgb_bytes\": %zu}\n", jpg.width,
+          jpg.height, jpg.components.size(), rgb.size());
   return 0;
 }
 
@@ -258,6 +304,8 @@ int Stages(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "encode")) return Encode(argc, argv);
   if (argc >= 2 && !strcmp(argv[1], "stages")) return Stages(argc, argv);
+  if (argc >= 2 && !strcmp(argv[1], "encode_jpeg")) return EncodeJpeg(argc, argv);
+  if (argc >= 2 && !strcmp(argv[1], "decode")) return Decode(argc, argv);
   fprintf(stderr,
           "usage: guetzli_ref encode RGB W H QUALITY OUT.jpg [c|cpu]\n"
           "       guetzli_ref stages RGB W H QSEED OUTDIR\n");
