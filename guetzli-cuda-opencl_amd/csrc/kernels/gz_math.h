@@ -287,8 +287,9 @@ __device__ __forceinline__ float clenshaw6(float x, float c0, float c1, float c2
 __device__ __forceinline__ f32x2 clenshaw6x2(float x, f32x2 c0, f32x2 c1, f32x2 c2, f32x2 c3,
                                              f32x2 c4, f32x2 c5) {
   const f32x2 xx = {x, x};
-  f32x2 b1 = {0.0f, 0.0f}, b2 = {0.0f, 0.0f}, xb, t;
-  xb = xx * b1; t = (xb + xb) - b2 + c5; b2 = b1; b1 = t;
+  // the first step from b1 = b2 = 0 gives exactly c5 for finite x
+  // ((x * 0 + x * 0) - 0 is a zero, and a zero plus c5 != 0 is c5)
+  f32x2 b1 = c5, b2 = {0.0f, 0.0f}, xb, t;
   xb = xx * b1; t = (xb + xb) - b2 + c4; b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + c3; b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + c2; b2 = b1; b1 = t;
@@ -297,10 +298,44 @@ __device__ __forceinline__ f32x2 clenshaw6x2(float x, f32x2 c0, f32x2 c1, f32x2 
   return xb - b2 + c0;
 }
 
+// Correctly rounded f32 division for operands in the normal range whose
+// quotient is normal (|a|, |b|, |a/b| within 2^-100 .. 2^100): the
+// compiler's IEEE sequence (v_div_scale, reciprocal + one Newton step, two
+// residual corrections, v_div_fmas, v_div_fixup) with the scale / fix-up
+// steps dropped -- they are the identity in that range (no operand or
+// quotient near the exponent limits, no zero, inf or NaN), so every value
+// is the one a / b gives.  Used where the operands are bounded by
+// construction (opsin absorbance >= 0.77, gamma values, MHIC mixing
+// denominators >= 106).
+__device__ __forceinline__ float fdiv_normal(float a, float b) {
+  float y = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  float q = a * y;
+  float r = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(r, y, q);
+  r = __builtin_fmaf(-b, q, a);
+  return __builtin_fmaf(r, y, q);
+}
+
+// (x - lo) / (hi - lo) of GammaPolynomialOpt as q = n * RN(1/d) plus one
+// residual correction: equal to the IEEE quotient for every numerator in
+// [2^-30, 2^10) (checked exhaustively over all floats of that range against
+// n / d on the host; tools/micro/div_probe.hip is the device form of the
+// check); here n = x - 0.77 with x the opsin absorbance, >= 0.774 and <= 256,
+// so n is 0 (exact either way) or >= 2^-24.
+__device__ __forceinline__ float fdiv_gamma_range(float n) {
+  constexpr float d = 274.579999999999984f - 0.770000000000000f;
+  constexpr float r = 1.0f / d;
+  const float q = n * r;
+  const float e = __builtin_fmaf(-q, d, n);
+  return __builtin_fmaf(e, r, q);
+}
+
 __device__ __forceinline__ float gamma_poly(float x) {
   // GammaPolynomialOpt, :861-874 (RationalPolynomialOpt :828-859)
-  const float lo = 0.770000000000000f, hi = 274.579999999999984f;
-  const float x01 = (x - lo) / (hi - lo);
+  const float lo = 0.770000000000000f;
+  const float x01 = fdiv_gamma_range(x - lo);
   // float(2.0 * double(x01) - 1.0) == 2.0f * x01 - 1.0f: the doubled value is
   // exact, and the difference is exact in double unless |2 x01| < 2^-29,
   // where both forms give -1.0f
@@ -314,8 +349,10 @@ __device__ __forceinline__ float gamma_poly(float x) {
                               f32x2{85.840860336314364f, 0.899112889751053f},
                               f32x2{6.683258861509244f, 0.035662329617191f});
   const float yp = r.x, yq = r.y;
-  if (yq == 0.0f) return 0.0f;
-  return yp / yq;
+  // (the denominator polynomial is >= 1.3 on [-1, 1]; the select keeps the
+  // reference's guard without a branch)
+  const float g = fdiv_normal(yp, yq);
+  return yq == 0.0f ? 0.0f : g;
 }
 
 // blurred: sigma-1.1 blur of the linear pixel; lin: the linear pixel.
@@ -324,7 +361,7 @@ __device__ __forceinline__ void opsin_pixel(const float blurred[3], const float 
   float pm[3], sens[3], cm[3];
   opsin_absorbance(blurred[0], blurred[1], blurred[2], pm);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) sens[c] = gamma_poly(pm[c]) / pm[c];
+  for (int c = 0; c < 3; ++c) sens[c] = fdiv_normal(gamma_poly(pm[c]), pm[c]);
   opsin_absorbance(lin[0], lin[1], lin[2], cm);
 #pragma unroll
   for (int c = 0; c < 3; ++c) cm[c] *= sens[c];
@@ -351,9 +388,10 @@ __device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], c
                                          float sqr_max_diff, float x0[3], float x1[3]) {
   const float kRX = 275.19165240059317f, kRY = 18599.41286306991f;
   const float kRZ = 410.8995306951065f, kChroma = 106.95800948271017f;
-  const float chroma_scale = kChroma / (ave[1] + kChroma);
-  const float mix[3] = {chroma_scale * kRX / (sqr_max_diff + kRX), kRY / (sqr_max_diff + kRY),
-                        chroma_scale * kRZ / (sqr_max_diff + kRZ)};
+  const float chroma_scale = fdiv_normal(kChroma, ave[1] + kChroma);
+  const float mix[3] = {fdiv_normal(chroma_scale * kRX, sqr_max_diff + kRX),
+                        fdiv_normal(kRY, sqr_max_diff + kRY),
+                        fdiv_normal(chroma_scale * kRZ, sqr_max_diff + kRZ)};
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     x0[c] = mix[c] * c0[c] + (1 - mix[c]) * ave[c];

@@ -20,7 +20,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libguetzli_hip.so")
+# GZ_LIB_PATH: an alternative build of the same library (A/B timing tools)
+LIB_PATH = os.environ.get("GZ_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libguetzli_hip.so")
 
 GZ_OK = 0
 _STATUS = {1: "invalid argument", 2: "device error", 3: "out of memory", 4: "unsupported",
