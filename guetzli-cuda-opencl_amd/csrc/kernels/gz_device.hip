@@ -229,6 +229,28 @@ inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
   }
   return dim3((bp.start[planes] + 3) / 4);
 }
+// Wave items of k_blur_vstream: per plane (64-column group, VsRows segment).
+inline int VStreamSegments(int sig, int h) {
+  switch (sig) {
+    case kSigLowFreq: return vstream_segments<kSigLowFreq>(h);
+    case kSigMaskX: return vstream_segments<kSigMaskX>(h);
+    case kSigMaskY: return vstream_segments<kSigMaskY>(h);
+    case kSigMaskB: return vstream_segments<kSigMaskB>(h);
+    case kSigMaskBSub: return vstream_segments<kSigMaskBSub>(h);
+    default: return vstream_segments<kSigDiffmap>(h);
+  }
+}
+inline dim3 BlurVStreamGrid(int w, int h, int planes, BlurPlanes& bp) {
+  bp.nplanes = planes;
+  bp.start[0] = 0;
+  for (int p = 0; p < planes; ++p) {
+    const int st = HostTables().blur[bp.sig[p]].step;
+    const int dx = (w + st - 1) / st;
+    bp.tiles[p] = (dx + kVsCols - 1) / kVsCols;
+    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * VStreamSegments(bp.sig[p], h);
+  }
+  return dim3((bp.start[planes] + 3) / 4);
+}
 // Outputs of one k_blur_h4 wave for a sigma.
 inline int H4Outputs(int sig) {
   switch (sig) {
@@ -640,8 +662,8 @@ bool Engine::MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b) {
     bp.in[c] = d_tmp_ + c * n_;
     bp.out[c] = d_ma_ + c * n_;
   }
-  const dim3 grid3 = BlurVLdsGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("mask_blur_v", k_blur_vlds<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+  const dim3 grid3 = BlurVStreamGrid(w_, h_, 3, bp);  // fills bp's packed-grid fields
+  GZ_TIMED("mask_blur_v", k_blur_vstream<kBlurMask><<<grid3, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
   return true;
 }
 
@@ -726,8 +748,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       bp.in[p] = d_tmp_ + p * n;
       bp.out[p] = d_bl_ + p * dn;
     }
-    const dim3 grid8 = BlurVLdsGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-    GZ_TIMED("lowfreq_blur_v", k_blur_vlds<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    const dim3 grid8 = BlurVStreamGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("lowfreq_blur_v", k_blur_vstream<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
@@ -759,8 +781,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
         RowsDiffmap{d_resval_, rw_}, bd, wc, hc, d_scales_, scale_stride_));
     bd.in[0] = d_tmp_;
     bd.out[0] = d_dd_;
-    const dim3 grid10 = BlurVLdsGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_v", k_blur_vlds<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
+    const dim3 grid10 = BlurVStreamGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
+    GZ_TIMED("diffmap_blur_v", k_blur_vstream<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
