@@ -270,7 +270,8 @@ inline dim3 BlurH4Grid(int w, int h, int planes, BlurPlanes& bp) {
     const int st = HostTables().blur[bp.sig[p]].step;
     const int dx = (w + st - 1) / st;
     bp.tiles[p] = (dx + H4Outputs(bp.sig[p]) - 1) / H4Outputs(bp.sig[p]);
-    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * h;
+    const int rep = bp.sig[p] == kSigDiffmap ? HRowRep<kSigDiffmap>::N : 1;
+    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * ((h + rep - 1) / rep);
   }
   return dim3((bp.start[planes] + 3) / 4);
 }
