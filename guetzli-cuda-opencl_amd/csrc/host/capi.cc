@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "host/jpeg_encode.h"
+#include "host/jpeg_reader.h"
 #include "host/jpeg_writer.h"
 #include "host/processor.h"
 #include "host/strips.h"
@@ -279,6 +280,18 @@ bool ValidCollectives(const gz_collectives* c) {
 }
 }  // namespace
 
+static gz_status Deliver(const gz::ProcessResult& res, uint8_t** jpeg_out, size_t* jpeg_size,
+                         gz_process_stats* stats);
+
+static gz::ProcessParams ToProcessParams(const gz_params* params) {
+  gz::ProcessParams pp;
+  pp.butteraugli_target = params->butteraugli_target;
+  pp.clear_metadata = params->clear_metadata != 0;
+  pp.zeroing_greedy_lookahead = params->zeroing_greedy_lookahead;
+  pp.new_zeroing_model = params->new_zeroing_model != 0;
+  return pp;
+}
+
 static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t* rgb,
                              bool device_ptr, int w, int h, uint8_t** jpeg_out,
                              size_t* jpeg_size, gz_process_stats* stats,
@@ -287,11 +300,7 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
     return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
   if (params->try_420 || params->force_420)
     return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output is not supported");
-  gz::ProcessParams pp;
-  pp.butteraugli_target = params->butteraugli_target;
-  pp.clear_metadata = params->clear_metadata != 0;
-  pp.zeroing_greedy_lookahead = params->zeroing_greedy_lookahead;
-  pp.new_zeroing_model = params->new_zeroing_model != 0;
+  const gz::ProcessParams pp = ToProcessParams(params);
   gz::ProcessResult res;
   std::string err;
   int rc;
@@ -302,6 +311,12 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
     rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
   }
   if (rc != 0) return SetError(rc, "process: " + err);
+  return Deliver(res, jpeg_out, jpeg_size, stats);
+}
+
+// The encoded bytes (library-allocated) and statistics of a finished encode.
+static gz_status Deliver(const gz::ProcessResult& res, uint8_t** jpeg_out, size_t* jpeg_size,
+                         gz_process_stats* stats) {
   uint8_t* buf = static_cast<uint8_t*>(std::malloc(res.jpeg.size() ? res.jpeg.size() : 1));
   if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "process: out of host memory");
   std::memcpy(buf, res.jpeg.data(), res.jpeg.size());
@@ -342,6 +357,52 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
                                 int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
                                 gz_process_stats* stats) {
   return ProcessImpl(device, params, rgb_dev, true, width, height, jpeg_out, jpeg_size, stats);
+}
+
+gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jpeg, size_t jpeg_len,
+                          uint8_t** jpeg_out, size_t* jpeg_size, gz_process_stats* stats) {
+  if (!params || !jpeg || !jpeg_out || !jpeg_size)
+    return SetError(GZ_ERR_INVALID_ARG, "process_jpeg: bad argument");
+  if (params->try_420 || params->force_420)
+    return SetError(GZ_ERR_UNSUPPORTED, "process_jpeg: 4:2:0 output is not supported");
+  gz::ProcessResult res;
+  std::string err;
+  const int rc = gz::ProcessJpeg(device, ToProcessParams(params), jpeg, jpeg_len, &res, &err);
+  if (rc != 0) return SetError(rc, "process_jpeg: " + err);
+  return Deliver(res, jpeg_out, jpeg_size, stats);
+}
+
+gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* height,
+                         int* ncomp, int16_t** coeffs_out, size_t* ncoeffs, uint8_t** rgb_out) {
+  if (!jpeg || !width || !height || !ncomp || !coeffs_out || !ncoeffs || !rgb_out)
+    return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: bad argument");
+  *coeffs_out = nullptr;
+  *rgb_out = nullptr;
+  gz::JpegData jpg;
+  std::string err;
+  if (!gz::ReadJpeg(jpeg, jpeg_len, &jpg, &err)) return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: " + err);
+  *width = jpg.width;
+  *height = jpg.height;
+  *ncomp = static_cast<int>(jpg.components.size());
+  size_t n = 0;
+  for (const auto& c : jpg.components) n += c.coeffs.size();
+  int16_t* co = static_cast<int16_t*>(std::malloc(n ? n * sizeof(int16_t) : 1));
+  if (!co) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
+  size_t at = 0;
+  for (const auto& c : jpg.components) {
+    std::memcpy(co + at, c.coeffs.data(), c.coeffs.size() * sizeof(int16_t));
+    at += c.coeffs.size();
+  }
+  *coeffs_out = co;
+  *ncoeffs = n;
+  std::vector<uint8_t> rgb;
+  if (gz::DecodeJpeg444ToRGB(jpg, &rgb)) {
+    uint8_t* r = static_cast<uint8_t*>(std::malloc(rgb.size()));
+    if (!r) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
+    std::memcpy(r, rgb.data(), rgb.size());
+    *rgb_out = r;
+  }
+  return GZ_OK;
 }
 
 gz_status gz_process_rgb_strips(int device, const gz_params* params, const uint8_t* rgb, int width,

@@ -17,6 +17,7 @@
 
 #include "guetzli_hip.h"
 #include "host/jpeg_encode.h"
+#include "host/jpeg_reader.h"
 #include "host/jpeg_writer.h"
 #include "host/lazy_sort.h"
 #include "host/thread_pool.h"
@@ -1097,6 +1098,57 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
       hrgb = host_rgb.data();
     }
     EncodeRGBToJpegData(hrgb, w, h, &jpg);
+  }
+  result->seconds_setup = Since(t0);
+  const int rc = ProcessJpegData(params, jpg, cmp.get(), result, err);
+  if (cmp) {
+    result->compares = cmp->compares;
+    result->seconds_compare = cmp->seconds_compare;
+    result->seconds_zeroing = cmp->seconds_zeroing;
+  }
+  result->seconds_total = Since(t0);
+  return rc;
+}
+
+int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, size_t len,
+                ProcessResult* result, std::string* err) {
+  // guetzli::Process(params, stats, data, jpg_out), processor.cc:1029-1066
+  const auto t0 = Clock::now();
+  JpegData jpg;
+  std::string rerr;
+  if (!ReadJpeg(data, len, &jpg, &rerr)) {
+    if (err) *err = "Can't read jpg data from input file: " + rerr;
+    return GZ_ERR_INVALID_ARG;
+  }
+  if (!CheckJpegSanity(jpg)) {
+    if (err) *err = "Unsupported input JPEG (unexpectedly large coefficient values)";
+    return GZ_ERR_INVALID_ARG;
+  }
+  // ProcessJpegData's input checks (processor.cc:946-963), ahead of the
+  // decode: this build has the 4:4:4 search only
+  if (jpg.components.size() != 3 || !HasYCbCrColorSpace(jpg)) {
+    if (err) *err = "Only YUV color space input jpeg is supported";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  if (!JpegIs444(jpg)) {
+    if (err) *err = JpegIs420(jpg) ? "4:2:0 input (the downsampling search) is not supported"
+                                   : "Unsupported sampling factors";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  std::vector<uint8_t> rgb;
+  if (!DecodeJpeg444ToRGB(jpg, &rgb)) {
+    if (err) *err = "input JPEG could not be decoded";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  std::unique_ptr<HipButteraugliComparator> cmp;
+  if (jpg.width >= 32 && jpg.height >= 32) {
+    std::string e;
+    cmp = HipButteraugliComparator::Create(device, jpg.width, jpg.height, rgb.data(), false,
+                                           params.butteraugli_target, &e);
+    if (!cmp) {
+      if (err) *err = e;
+      return GZ_ERR_DEVICE;
+    }
   }
   result->seconds_setup = Since(t0);
   const int rc = ProcessJpegData(params, jpg, cmp.get(), result, err);

@@ -195,6 +195,13 @@ struct ProcessResult {
 int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool device_ptr, int w,
             int h, ProcessResult* result, std::string* err);
 
+// guetzli::Process(params, stats, jpeg_bytes, out) (processor.cc:1029-1066):
+// ReadJpeg, CheckJpegSanity, DecodeJpegToRGB as the comparator's reference,
+// ProcessJpegData on the input's own coefficients.  4:4:4 YCbCr inputs;
+// 4:2:0 (the reference's downsampling path) returns GZ_ERR_UNSUPPORTED.
+int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, size_t len,
+                ProcessResult* result, std::string* err);
+
 // The q=1 4:4:4 JPEG model of an RGB image (EncodeRGBToJpeg).
 void EncodeRGBToJpegData(const uint8_t* rgb, int w, int h, JpegData* jpg);
 

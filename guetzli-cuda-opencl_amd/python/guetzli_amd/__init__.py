@@ -75,7 +75,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_original_coeffs", "gz_comparator_write_jpeg", "gz_write_jpeg_host",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
-    "gz_collectives_selftest",
+    "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode",
 )
 
 _lib = None
@@ -108,6 +108,12 @@ def lib():
     L.gz_butteraugli_score_for_quality.argtypes = [ctypes.c_double]
     L.gz_butteraugli_score_for_quality.restype = ctypes.c_double
     L.gz_free.argtypes = [vp]
+    L.gz_process_jpeg.argtypes = [i32, ctypes.POINTER(_Params), vp, ctypes.c_size_t,
+                                  ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t),
+                                  ctypes.POINTER(_Stats)]
+    L.gz_jpeg_decode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                 ctypes.POINTER(i32), ctypes.POINTER(vp),
+                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(vp)]
     for name in ("gz_process_rgb", "gz_process_rgb_device"):
         fn = getattr(L, name)
         fn.argtypes = [i32, ctypes.POINTER(_Params), vp, i32, i32, ctypes.POINTER(vp),
@@ -295,6 +301,50 @@ def process(rgb, width, height, params=None, device=0, return_stats=False):
                                   st.seconds_total, st.seconds_setup, st.seconds_write,
                                   st.seconds_quantize, st.seconds_backend)
     return data
+
+
+def process_jpeg(jpeg, params=None, device=0, return_stats=False):
+    """guetzli::Process on JPEG file bytes (processor.cc:1029-1066) -> JPEG
+    bytes.  4:4:4 YCbCr inputs; others raise GuetzliError(GZ_ERR_UNSUPPORTED)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(bytes(jpeg), len(jpeg))
+    p = (params or Params())._c()
+    out = ctypes.c_void_p()
+    size = ctypes.c_size_t()
+    st = _Stats()
+    _check(L.gz_process_jpeg(device, ctypes.byref(p), ctypes.cast(buf, ctypes.c_void_p), len(jpeg),
+                             ctypes.byref(out), ctypes.byref(size), ctypes.byref(st)),
+           "process_jpeg")
+    data = ctypes.string_at(out, size.value)
+    L.gz_free(out)
+    if return_stats:
+        return data, ProcessStats(st.iterations, st.iterations_up, st.iterations_down,
+                                  st.compares, st.seconds_compare, st.seconds_zeroing,
+                                  st.seconds_total, st.seconds_setup, st.seconds_write,
+                                  st.seconds_quantize, st.seconds_backend)
+    return data
+
+
+def jpeg_decode(jpeg):
+    """ReadJpeg + DecodeJpegToRGB (host only): returns (width, height, ncomp,
+    int16 quantized coefficients of all components concatenated, RGB8 array
+    of shape (h, w, 3) for 4:4:4 YCbCr inputs or None)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(bytes(jpeg), len(jpeg))
+    w, h, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    co, rgb = ctypes.c_void_p(), ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    _check(L.gz_jpeg_decode(ctypes.cast(buf, ctypes.c_void_p), len(jpeg), ctypes.byref(w),
+                            ctypes.byref(h), ctypes.byref(nc), ctypes.byref(co), ctypes.byref(n),
+                            ctypes.byref(rgb)), "jpeg_decode")
+    coeffs = np.frombuffer(ctypes.string_at(co, 2 * n.value), np.int16).copy()
+    L.gz_free(co)
+    img = None
+    if rgb.value:
+        img = np.frombuffer(ctypes.string_at(rgb, 3 * w.value * h.value), np.uint8).reshape(
+            h.value, w.value, 3).copy()
+        L.gz_free(rgb)
+    return w.value, h.value, nc.value, coeffs, img
 
 
 def process_device(rgb_dev_ptr, width, height, params=None, device=0, return_stats=False):

@@ -114,6 +114,23 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
                                 int width, int height, uint8_t** jpeg_out, size_t* jpeg_size,
                                 gz_process_stats* stats);
 
+/* Encodes a JPEG file: guetzli::Process(params, stats, jpeg_bytes, out)
+ * (guetzli/processor.h:44-46, processor.cc:1029-1066) -- the input's own
+ * coefficients and quantization start the search, its decoded pixels are the
+ * Butteraugli reference.  Baseline / extended / progressive Huffman JPEGs with
+ * 4:4:4 YCbCr sampling; 4:2:0 and other layouts return GZ_ERR_UNSUPPORTED,
+ * unreadable input GZ_ERR_INVALID_ARG.  *jpeg_out: library-allocated
+ * (gz_free). */
+gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jpeg, size_t jpeg_len,
+                          uint8_t** jpeg_out, size_t* jpeg_size, gz_process_stats* stats);
+/* ReadJpeg (guetzli/jpeg_data_reader.cc:931-1079, JPEG_READ_ALL) and
+ * DecodeJpegToRGB (jpeg_data_decoder.cc:45-55) of a JPEG file, host only:
+ * *coeffs_out the quantized coefficients of every component ([comp][blocks]
+ * [64], natural order, MCU-padded grid; *ncoeffs values), *rgb_out the RGB8
+ * image for 4:4:4 YCbCr inputs, else NULL.  Both library-allocated (gz_free). */
+gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* height,
+                         int* ncomp, int16_t** coeffs_out, size_t* ncoeffs, uint8_t** rgb_out);
+
 /* ---- one frame over several GPUs (row strips + halo) ------------------ */
 /* The exchange a multi-rank encode needs: an equal-size all-gather (every
  * rank contributes `bytes` bytes, `recv` receives world*bytes in rank order);

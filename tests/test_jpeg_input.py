@@ -1,0 +1,86 @@
+"""JPEG input: guetzli::Process on a JPEG file (processor.cc:1029-1066).
+
+The reader (ReadJpeg, jpeg_data_reader.cc) and the 4:4:4 decode
+(DecodeJpegToRGB, jpeg_data_decoder.cc:45-55) are host code, checked on the
+CPU against the reference's own answers on the committed inputs
+(tests/golden/jpeg/, made by tests/golden/make_jpeg_fixtures.py: baseline,
+optimized-Huffman with restart markers, progressive, 4:2:0, a guetzli
+output): sha256 of the quantized coefficients and of the decoded RGB.  The
+encode itself runs on the GPU and must reproduce the reference's bytes.
+"""
+import hashlib
+import json
+import os
+
+import pytest
+
+import guetzli_amd as gz
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = json.load(open(os.path.join(GOLDEN, "manifest.json")))["jpeg"]
+
+
+def _data(name):
+    return open(os.path.join(GOLDEN, CASES[name]["input"]), "rb").read()
+
+
+def _sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_read_and_decode_match_reference(name):
+    e = CASES[name]
+    data = _data(name)
+    assert _sha(data) == e["input_sha256"]
+    w, h, nc, coeffs, rgb = gz.jpeg_decode(data)
+    assert (w, h, nc) == (e["w"], e["h"], 3)
+    assert _sha(coeffs.tobytes()) == e["coeffs_sha256"]
+    if "_420" in name:
+        assert rgb is None  # the 4:2:0 decode (fancy upsampling) is not built
+    else:
+        assert _sha(rgb.tobytes()) == e["rgb_sha256"]
+
+
+def test_progressive_input_decodes_ac_coefficients():
+    # the progressive file's AC bands come from first + refinement scans
+    w, h, _, co, rgb = gz.jpeg_decode(_data("synth_pil_q85_444_prog"))
+    assert rgb.shape == (h, w, 3)
+    assert (co.reshape(3, -1, 64)[:, :, 1:] != 0).any()
+
+
+@pytest.mark.parametrize("bad", [b"", b"\xff\xd8", b"not a jpeg at all",
+                                 "truncated", "no_eoi_scan"])
+def test_reader_rejects_invalid_input(bad):
+    if bad == "truncated":
+        bad = _data("bees_pil_q90_444")[:600]
+    elif bad == "no_eoi_scan":
+        d = _data("tiny_pil_q85_444")
+        bad = d[:d.index(b"\xff\xda")]  # headers only
+    with pytest.raises(gz.GuetzliError) as ei:
+        gz.jpeg_decode(bad)
+    assert ei.value.status == 1  # GZ_ERR_INVALID_ARG
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(n for n in CASES if "_420" not in n))
+def test_process_jpeg_matches_reference(name):
+    e = CASES[name]
+    assert e["reference_ok"]
+    out, st = gz.process_jpeg(_data(name), gz.Params.for_quality(e["quality"]), return_stats=True)
+    assert len(out) == e["bytes"]
+    assert _sha(out) == e["sha256"]
+
+
+@pytest.mark.gpu
+def test_process_jpeg_420_is_unsupported():
+    with pytest.raises(gz.GuetzliError) as ei:
+        gz.process_jpeg(_data("synth_pil_q85_420"), gz.Params.for_quality(95))
+    assert ei.value.status == 4  # GZ_ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_process_jpeg_rejects_garbage():
+    with pytest.raises(gz.GuetzliError) as ei:
+        gz.process_jpeg(b"\xff\xd8\xff\xe0garbage", gz.Params.for_quality(95))
+    assert ei.value.status == 1
