@@ -76,14 +76,14 @@ BLUR_MASK_STAGES = ("opsin_mhic", "edge_blur", "lowfreq_blur_h",
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
 STAGE_SYMBOL = {
-    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_mhic": "gz::k_opsin_mhic(",
+    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_mhic": "gz::k_opsin_mhic_stream(",
     "edge_blur": "void gz::k_blur_stream<2>(", "edge_map": "gz::k_edge_map(",
-    "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h_tiled<3,",
-    "lowfreq_blur_v": "void gz::k_blur_vcol<3>(", "low_freq": "gz::k_low_freq(",
+    "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
+    "lowfreq_blur_v": "void gz::k_blur_vstream<3>(", "low_freq": "gz::k_low_freq(",
     "mask_front": "gz::k_mask_stream(",
-    "mask_blur_h": "void gz::k_blur_h_tiled<4,", "mask_blur_v": "void gz::k_blur_vcol<4>(",
-    "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h_tiled<5,",
-    "diffmap_blur_v": "void gz::k_blur_vcol<5>(", "diffmap_final": "gz::k_diffmap_final(",
+    "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
+    "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
+    "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
 }
 
 
@@ -307,6 +307,12 @@ def main():
                      "achieved_GBps": round(bm_bytes / (bm_ms * 1e-3) / 1e9, 1),
                      "frac": round(bm_bytes / (bm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "stages": [k for k in BLUR_MASK_STAGES if k in stages]}
+        # measured HBM bytes of the same launches (committed PMC summary of
+        # this frame size), where every stage has one
+        tr = [measured_traffic(k, w, h)[0] for k in blur_mask["stages"]]
+        if tr and all(t is not None for t in tr):
+            blur_mask["traffic"] = int(sum(tr))
+            blur_mask["traffic_GBps"] = round(sum(tr) / (bm_ms * 1e-3) / 1e9, 1)
     cp = prof.get("compare_pass")
     pass_bytes = sum(bpp.values()) * w * h
     compare_pass = None

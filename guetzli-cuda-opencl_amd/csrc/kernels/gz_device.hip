@@ -172,31 +172,6 @@ inline dim3 PixGrid(int w, int h, int planes = 1) {
   return dim3((w + 255) / 256, h, planes);
 }
 
-// Packs the planes' (tile, row) work items of a blur pass into one 1-D grid
-// (planes of different steps have different output sizes; no idle groups).
-inline dim3 PackBlurGrid(BlurPlanes* bp, int planes, int w, int h, bool vertical) {
-  bp->nplanes = planes;
-  bp->start[0] = 0;
-  for (int p = 0; p < planes; ++p) {
-    const int st = HostTables().blur[bp->sig[p]].step;
-    const int dx = (w + st - 1) / st;
-    bp->tiles[p] = (dx + 255) / 256;
-    const int rows = vertical ? (h + st - 1) / st : h;
-    bp->start[p + 1] = bp->start[p] + bp->tiles[p] * rows;
-  }
-  return dim3(bp->start[planes]);
-}
-// Wave items of k_blur_vcol: per plane (64-column group, row segment).
-inline int VColSegments(int sig, int h) {
-  switch (sig) {
-    case kSigLowFreq: return vcol_segments<kSigLowFreq>(h);
-    case kSigMaskX: return vcol_segments<kSigMaskX>(h);
-    case kSigMaskY: return vcol_segments<kSigMaskY>(h);
-    case kSigMaskB: return vcol_segments<kSigMaskB>(h);
-    case kSigMaskBSub: return vcol_segments<kSigMaskBSub>(h);
-    default: return vcol_segments<kSigDiffmap>(h);
-  }
-}
 // The blurred mask planes (in down-sampled form) at base + c * n.
 inline MaskPlanes MaskPlanesOf(const float* base, size_t n, bool sub_b) {
   MaskPlanes mk{};
@@ -205,29 +180,6 @@ inline MaskPlanes MaskPlanesOf(const float* base, size_t n, bool sub_b) {
     mk.step[c] = HostTables().blur[c == 2 && sub_b ? kSigMaskBSub : kSigMaskX + c].step;
   }
   return mk;
-}
-// Workgroups of k_blur_vlds: per plane (64-column group, kVlOut-row segment).
-inline dim3 BlurVLdsGrid(int w, int h, int planes, BlurPlanes& bp) {
-  bp.nplanes = planes;
-  bp.start[0] = 0;
-  for (int p = 0; p < planes; ++p) {
-    const int st = HostTables().blur[bp.sig[p]].step;
-    const int dx = (w + st - 1) / st, dy = (h + st - 1) / st;
-    bp.tiles[p] = (dx + 63) / 64;
-    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * ((dy + kVlOut - 1) / kVlOut);
-  }
-  return dim3(bp.start[planes]);
-}
-inline dim3 BlurVColGrid(int w, int h, int planes, BlurPlanes& bp) {
-  bp.nplanes = planes;
-  bp.start[0] = 0;
-  for (int p = 0; p < planes; ++p) {
-    const int st = HostTables().blur[bp.sig[p]].step;
-    const int dx = (w + st - 1) / st;
-    bp.tiles[p] = (dx + 63) / 64;
-    bp.start[p + 1] = bp.start[p] + bp.tiles[p] * VColSegments(bp.sig[p], h);
-  }
-  return dim3((bp.start[planes] + 3) / 4);
 }
 // Wave items of k_blur_vstream: per plane (64-column group, VsRows segment).
 inline int VStreamSegments(int sig, int h) {
@@ -275,8 +227,6 @@ inline dim3 BlurH4Grid(int w, int h, int planes, BlurPlanes& bp) {
   }
   return dim3((bp.start[planes] + 3) / 4);
 }
-inline dim3 BlurHGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, false); }
-inline dim3 BlurVGrid(int w, int h, int planes, BlurPlanes& bp) { return PackBlurGrid(&bp, planes, w, h, true); }
 inline RowsPlain Rows(const BlurPlanes& bp, int w) {
   RowsPlain r{};
   for (int p = 0; p < 6; ++p) r.in[p] = bp.in[p];
