@@ -13,3 +13,11 @@ timeout -k 10 600 python bench.py > gpurun_out/round_bench.json 2> gpurun_out/ro
 head -c 600 gpurun_out/round_bench.json; echo
 GZ_PROF_TAG=prof1080 bash tools/gpu_profile.sh || exit $?
 GZ_PROF_W=3840 GZ_PROF_H=2160 GZ_PROF_TAG=prof4k GZ_PROF_BENCH_ARGS="--quality 90" bash tools/gpu_profile.sh || exit $?
+mkdir -p gpurun_out/util
+for sz in "1920 1080" "3840 2160"; do
+  set -- $sz
+  rm -rf gpurun_out/pmck
+  GZ_PMC_ARGS="--width $1 --height $2 --compares 3" bash tools/gpu_pmc_kernels.sh > /dev/null 2>&1 || exit $?
+  python tools/pmc_summary.py gpurun_out/pmck --json > gpurun_out/util/pmc_util_$1x$2.json || exit $?
+  echo "pmc util $1x$2 ok"
+done

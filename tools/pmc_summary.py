@@ -13,6 +13,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--filter", default="")
+    ap.add_argument("--json", action="store_true", help="per-dispatch averages as JSON")
     args = ap.parse_args()
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(lambda: collections.defaultdict(int))
@@ -20,7 +21,7 @@ def main():
     for f in glob.glob(os.path.join(args.root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                k = row["Kernel_Name"].split("(")[0][:48]
+                k = row["Kernel_Name"].split("(")[0] if args.json else row["Kernel_Name"].split("(")[0][:48]
                 if args.filter not in k:
                     continue
                 c = row["Counter_Name"]
@@ -28,6 +29,14 @@ def main():
                 acc[k][c] += float(row["Counter_Value"])
                 cnt[k][(c, row.get("Dispatch_Id", ""))] = 1
     cols = sorted(names)
+    if args.json:
+        import json
+        out = {}
+        for k in sorted(acc):
+            nd = max(1, len({d for (c, d) in cnt[k] if c == cols[0]}))
+            out[k] = {c: acc[k][c] / nd for c in cols}
+        print(json.dumps(out, indent=1, sort_keys=True))
+        return
     print("kernel".ljust(48), " ".join(c[3:15].rjust(12) for c in cols))
     for k in sorted(acc):
         nd = max(1, len({d for (c, d) in cnt[k] if c == cols[0]}))
