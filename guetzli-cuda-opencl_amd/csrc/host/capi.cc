@@ -396,7 +396,7 @@ gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* 
   *coeffs_out = co;
   *ncoeffs = n;
   std::vector<uint8_t> rgb;
-  if (gz::DecodeJpeg444ToRGB(jpg, &rgb)) {
+  if (gz::DecodeJpegToRGB(jpg, &rgb)) {
     uint8_t* r = static_cast<uint8_t*>(std::malloc(rgb.size()));
     if (!r) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
     std::memcpy(r, rgb.data(), rgb.size());

@@ -29,10 +29,11 @@ bool HasYCbCrColorSpace(const JpegData& jpg);
 // CheckJpegSanity, processor.cc:118-131: |coeff * quant| <= 4096
 bool CheckJpegSanity(const JpegData& jpg);
 
-// DecodeJpegToRGB for a 3-component YCbCr 4:4:4 image: dequantize, the
-// integer IDCT of idct.cc:139-161 and the YCbCr -> RGB tables of
-// color_transform.h (OutputImage::CopyFromJpegData + ToSRGB).  False for any
-// other layout.
-bool DecodeJpeg444ToRGB(const JpegData& jpg, std::vector<uint8_t>* rgb);
+// DecodeJpegToRGB (jpeg_data_decoder.cc:45-55) for 3-component YCbCr 4:4:4
+// and 4:2:0 images: OutputImage::CopyFromJpegData (dequantize, the integer
+// IDCT of idct.cc:139-161, the fancy upsampler of output_image.cc:135-205 for
+// the subsampled chroma) + ToSRGB.  False for any other layout (the reference
+// returns an empty image there).
+bool DecodeJpegToRGB(const JpegData& jpg, std::vector<uint8_t>* rgb);
 
 }  // namespace gz

@@ -1136,7 +1136,7 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     return GZ_ERR_UNSUPPORTED;
   }
   std::vector<uint8_t> rgb;
-  if (!DecodeJpeg444ToRGB(jpg, &rgb)) {
+  if (!DecodeJpegToRGB(jpg, &rgb)) {
     if (err) *err = "input JPEG could not be decoded";
     return GZ_ERR_UNSUPPORTED;
   }

@@ -328,7 +328,7 @@ def process_jpeg(jpeg, params=None, device=0, return_stats=False):
 def jpeg_decode(jpeg):
     """ReadJpeg + DecodeJpegToRGB (host only): returns (width, height, ncomp,
     int16 quantized coefficients of all components concatenated, RGB8 array
-    of shape (h, w, 3) for 4:4:4 YCbCr inputs or None)."""
+    of shape (h, w, 3) for 4:4:4 / 4:2:0 YCbCr inputs, else None)."""
     L = lib()
     buf = ctypes.create_string_buffer(bytes(jpeg), len(jpeg))
     w, h, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

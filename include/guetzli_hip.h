@@ -127,7 +127,7 @@ gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jp
  * DecodeJpegToRGB (jpeg_data_decoder.cc:45-55) of a JPEG file, host only:
  * *coeffs_out the quantized coefficients of every component ([comp][blocks]
  * [64], natural order, MCU-padded grid; *ncoeffs values), *rgb_out the RGB8
- * image for 4:4:4 YCbCr inputs, else NULL.  Both library-allocated (gz_free). */
+ * image for 4:4:4 and 4:2:0 YCbCr inputs, else NULL.  Both library-allocated (gz_free). */
 gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* height,
                          int* ncomp, int16_t** coeffs_out, size_t* ncoeffs, uint8_t** rgb_out);
 
