@@ -927,19 +927,18 @@ bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, u
   GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_));
   if (!ScanCounts(d_jbitlen_, nb_, d_jbitoff_, "jpeg_scan")) return false;
   // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any scan)
-  GZ_HIP(hipMemsetAsync(d_jinfo_, 0, 4, s));
-  GZ_TIMED("jpeg_emit", (k_zero_words<<<512, 256, 0, s>>>(d_jbitoff_ + nb_, words),
+  GZ_TIMED("jpeg_emit", (k_zero_words<<<512, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_),
                          k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
                          k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_)));
-  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jbitoff_ + nb_, 4, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 3, d_jinfo_, 4, hipMemcpyDeviceToHost, s));
+  // (0xff count, bit total) in one read
+  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jinfo_, 8, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
-  const uint64_t total = h_jhist_[6 * 256 + 2];
+  const uint64_t total = static_cast<uint32_t>(h_jhist_[6 * 256 + 3]);
   if ((total + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
   jnbits_[jslot_] = total;
   *nbits = total;
-  *ff = h_jhist_[6 * 256 + 3];
+  *ff = h_jhist_[6 * 256 + 2];
   return true;
 }
 
