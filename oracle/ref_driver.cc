@@ -103,13 +103,14 @@ int Encode(int argc, char** argv) {
 }
 
 // guetzli::Process on a JPEG file (processor.cc:1029-1066), --c mode:
-//   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg
+//   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg [keep]   (keep: clear_metadata = false)
 int EncodeJpeg(int argc, char** argv) {
   if (argc < 5) return 1;
   std::vector<uint8_t> in = ReadAll(argv[2]);
   const int quality = atoi(argv[3]);
   g_mathMode = MODE_CPU_OPT;
   guetzli::Params params;
+  if (argc > 5 && !strcmp(argv[5], "keep")) params.clear_metadata = false;
   params.butteraugli_target =
       static_cast<float>(guetzli::ButteraugliScoreForQuality(quality));
   guetzli::ProcessStats stats;

@@ -53,6 +53,11 @@ def inputs():
         # 4:2:0 and progressive: the reference handles them, this build does not
         "synth_pil_q85_420": (pil_jpeg(synth, quality=85, subsampling=2), 95),
         "synth_pil_q85_444_prog": (pil_jpeg(synth, quality=85, subsampling=0, progressive=True), 95),
+        # APP1 (Exif) + COM segments, encoded with clear_metadata = false
+        # (the input's APPn / COM are carried to the output)
+        "synth_pil_q85_444_meta": (pil_jpeg(synth, quality=85, subsampling=0,
+                                            exif=b"Exif\x00\x00MM\x00*\x00\x00\x00\x08\x00\x00",
+                                            comment=b"guetzli-mi355x fixture"), 95),
     }
     # a guetzli output as input (SOF1, guetzli's own table layout)
     tmp = tempfile.mkdtemp()
@@ -83,8 +88,11 @@ def main():
                      rgb_sha256=hashlib.sha256(open(rgb_p, "rb").read()).hexdigest(),
                      coeffs_sha256=hashlib.sha256(open(co_p, "rb").read()).hexdigest())
         out_p = os.path.join(tmp, "o.jpg")
-        r = subprocess.run([REF, "encode_jpeg", path, str(quality), out_p], capture_output=True,
-                           text=True)
+        keep = name.endswith("_meta")
+        if keep:
+            e["clear_metadata"] = False
+        r = subprocess.run([REF, "encode_jpeg", path, str(quality), out_p] + (["keep"] if keep else []),
+                           capture_output=True, text=True)
         e["reference_ok"] = r.returncode == 0
         if r.returncode == 0:
             info = json.loads(r.stdout)

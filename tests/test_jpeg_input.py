@@ -64,7 +64,8 @@ def test_reader_rejects_invalid_input(bad):
 def test_process_jpeg_matches_reference(name):
     e = CASES[name]
     assert e["reference_ok"]
-    out, st = gz.process_jpeg(_data(name), gz.Params.for_quality(e["quality"]), return_stats=True)
+    params = gz.Params.for_quality(e["quality"], clear_metadata=e.get("clear_metadata", True))
+    out, st = gz.process_jpeg(_data(name), params, return_stats=True)
     assert len(out) == e["bytes"]
     assert _sha(out) == e["sha256"]
 
