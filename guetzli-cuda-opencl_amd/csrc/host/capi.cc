@@ -156,14 +156,15 @@ gz_status gz_comparator_start_block_comparisons(gz_comparator* cmp, float* mask_
 
 gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* cur_coeffs,
                                              const int16_t* orig_coeffs, int comp_mask,
-                                             float limit, int lookahead, gz_coeff_data* out) {
+                                             float limit, int lookahead, int new_zeroing_model,
+                                             gz_coeff_data* out) {
   if (!cmp || !cur_coeffs || !orig_coeffs || !out || lookahead < 1 || comp_mask <= 0 ||
       comp_mask > 7)
     return SetError(GZ_ERR_INVALID_ARG, "block_zeroing_orders: bad argument");
   gz::Engine& e = *cmp->engine;
   static_assert(sizeof(gz_coeff_data) == sizeof(gz::CoeffDataHost), "CoeffData layout");
   if (!e.SetOriginalCoeffs(orig_coeffs, false) || !e.UploadCoeffs(cur_coeffs) ||
-      !e.BlockZeroingOrders(comp_mask, limit, lookahead,
+      !e.BlockZeroingOrders(comp_mask, limit, lookahead, new_zeroing_model != 0,
                             reinterpret_cast<gz::CoeffDataHost*>(out)))
     return SetError(GZ_ERR_DEVICE, "block_zeroing_orders: " + e.error());
   return GZ_OK;
@@ -257,6 +258,37 @@ gz_status gz_rgb_to_coeffs(const uint8_t* rgb, int width, int height, int16_t* c
       height >= (1 << 16))
     return SetError(GZ_ERR_INVALID_ARG, "rgb_to_coeffs: bad argument");
   gz::RgbToCoeffsQ1(rgb, width, height, coeffs_out);
+  return GZ_OK;
+}
+
+size_t gz_engine_pool_trim(size_t keep_bytes) { return gz::TrimEnginePool(keep_bytes); }
+
+size_t gz_engine_pool_idle_bytes(void) { return gz::EnginePoolIdleBytes(); }
+
+gz_status gz_block_error_adjustment_weights(int width, int height, float target, int direction,
+                                            int max_block_dist, double target_mul, int factor_x,
+                                            int factor_y, const float* distmap,
+                                            float* block_weight) {
+  if (!distmap || !block_weight || width <= 0 || height <= 0 || factor_x < 1 || factor_y < 1 ||
+      (direction != 1 && direction != -1) || max_block_dist < 0)
+    return SetError(GZ_ERR_INVALID_ARG, "block_error_adjustment_weights: bad argument");
+  // per-block maxima of the distance map (butteraugli_comparator.cc:181-195),
+  // then the weights from them (the search loop gets the maxima from the device)
+  const int sx = 8 * factor_x, sy = 8 * factor_y;
+  const int bw = (width + sx - 1) / sx, bh = (height + sy - 1) / sy;
+  std::vector<float> bmax(static_cast<size_t>(bw) * bh);
+  for (int by = 0; by < bh; ++by)
+    for (int bx = 0; bx < bw; ++bx) {
+      float m = 0.0f;
+      for (int y = sy * by; y < std::min(height, sy * (by + 1)); ++y)
+        for (int x = sx * bx; x < std::min(width, sx * (bx + 1)); ++x)
+          m = std::max(m, distmap[static_cast<size_t>(y) * width + x]);
+      bmax[static_cast<size_t>(by) * bw + bx] = m;
+    }
+  std::vector<float> wgt(block_weight, block_weight + bmax.size());
+  gz::BlockErrorAdjustmentWeights(width, height, target, direction, max_block_dist, target_mul,
+                                  factor_x, factor_y, bmax, &wgt);
+  std::copy(wgt.begin(), wgt.end(), block_weight);
   return GZ_OK;
 }
 

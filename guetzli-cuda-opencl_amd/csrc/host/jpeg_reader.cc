@@ -128,7 +128,9 @@ struct Reader {
       c.width_in_blocks = jpg->mcu_cols * c.h_samp_factor;
       c.height_in_blocks = jpg->mcu_rows * c.v_samp_factor;
       const uint64_t nb = static_cast<uint64_t>(c.width_in_blocks) * c.height_in_blocks;
-      if (nb > (1ull << 26)) return Fail("image too large");
+      // JPEG_IMAGE_TOO_LARGE above 2M blocks per component, as the reference
+      // (jpeg_data_reader.cc:151-158): checked before any allocation
+      if (nb > (1ull << 21)) return Fail("image too large");
       c.coeffs.assign(nb * 64, 0);
     }
     return pos == start + mlen || Fail("bad SOF length");

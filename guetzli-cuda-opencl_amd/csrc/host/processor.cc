@@ -298,13 +298,13 @@ bool HipButteraugliComparator::StartBlockComparisons() {
 }
 
 bool HipButteraugliComparator::BlockZeroingOrders(const CoeffImage& img, const JpegData&,
-                                                  int comp_mask, int lookahead,
+                                                  int comp_mask, int lookahead, bool new_model,
                                                   std::vector<CoeffData>* out) {
   const auto t0 = Clock::now();
   if (!SyncCoeffs(img)) return false;
   out->resize(static_cast<size_t>(img.blocks) * 192);
   static_assert(sizeof(CoeffData) == sizeof(CoeffDataHost), "CoeffData layout");
-  if (!engine_->BlockZeroingOrders(comp_mask, target_, lookahead,
+  if (!engine_->BlockZeroingOrders(comp_mask, target_, lookahead, new_model,
                                    reinterpret_cast<CoeffDataHost*>(out->data()))) {
     err_ = engine_->error();
     return false;
@@ -314,10 +314,11 @@ bool HipButteraugliComparator::BlockZeroingOrders(const CoeffImage& img, const J
 }
 
 bool Comparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg,
-                                        int comp_mask, int lookahead, std::vector<int>* offsets,
-                                        std::vector<uint8_t>* idx, std::vector<float>* err) {
+                                        int comp_mask, int lookahead, bool new_model,
+                                        std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                                        std::vector<float>* err) {
   std::vector<CoeffData> order;
-  if (!BlockZeroingOrders(img, orig_jpg, comp_mask, lookahead, &order)) return false;
+  if (!BlockZeroingOrders(img, orig_jpg, comp_mask, lookahead, new_model, &order)) return false;
   const float limit = BlockErrorLimit();
   offsets->assign(img.blocks + 1, 0);
   idx->clear();
@@ -337,13 +338,14 @@ bool Comparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData& o
 }
 
 bool HipButteraugliComparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData&,
-                                                      int comp_mask, int lookahead,
+                                                      int comp_mask, int lookahead, bool new_model,
                                                       std::vector<int>* offsets,
                                                       std::vector<uint8_t>* idx,
                                                       std::vector<float>* err) {
   const auto t0 = Clock::now();
   if (!SyncCoeffs(img)) return false;
-  if (!engine_->BlockZeroingCandidates(comp_mask, target_, lookahead, offsets, idx, err)) {
+  if (!engine_->BlockZeroingCandidates(comp_mask, target_, lookahead, new_model, offsets, idx,
+                                       err)) {
     err_ = engine_->error();
     return false;
   }
@@ -784,6 +786,7 @@ bool Processor::SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int
   std::vector<uint8_t> cand;
   std::vector<float> cand_err;
   if (!cmp_->BlockZeroingCandidates(*img, jpg, comp_mask, params_.zeroing_greedy_lookahead,
+                                    params_.new_zeroing_model,
                                     &offsets, &cand, &cand_err))
     return Fail(err);
   cmp_->FinishBlockComparisons();

@@ -37,13 +37,15 @@ class Comparator {
   virtual bool Compare(const CoeffImage& img) = 0;
   virtual bool StartBlockComparisons() = 0;
   virtual void FinishBlockComparisons() = 0;
+  // lookahead / new_model: Params::zeroing_greedy_lookahead / new_zeroing_model.
   virtual bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
-                                  int lookahead, std::vector<CoeffData>* out) = 0;
+                                  int lookahead, bool new_model, std::vector<CoeffData>* out) = 0;
   // The back end's input: per block the BlockZeroingOrders entries with
   // 0 < block_err <= BlockErrorLimit(), in order, concatenated (offsets has
   // blocks + 1 entries) -- processor.cc:690-700.  Default: filter the orders.
   virtual bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg,
-                                      int comp_mask, int lookahead, std::vector<int>* offsets,
+                                      int comp_mask, int lookahead, bool new_model,
+                                      std::vector<int>* offsets,
                                       std::vector<uint8_t>* idx, std::vector<float>* err);
   // CopyFromJpegData(q=1) + ApplyGlobalQuantization(q) of the originals into img
   // (and into any device mirror).
@@ -120,9 +122,10 @@ class HipButteraugliComparator : public Comparator {
   bool StartBlockComparisons() override;
   void FinishBlockComparisons() override {}
   bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
-                          int lookahead, std::vector<CoeffData>* out) override;
+                          int lookahead, bool new_model, std::vector<CoeffData>* out) override;
   bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
-                              int lookahead, std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                              int lookahead, bool new_model, std::vector<int>* offsets,
+                              std::vector<uint8_t>* idx,
                               std::vector<float>* err) override;
   bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
                             bool need_host = true) override;

@@ -142,26 +142,53 @@ bool StripComparator::QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffI
   return true;
 }
 
-bool StripComparator::Compare(const CoeffImage& img) {
-  if (!Sync(img)) return false;
-  std::vector<float> mine(max_owned_, 0.0f);
-  if (inner_) {
-    if (!inner_->Compare(local_)) return Fail(inner_->error());
-    const std::vector<float>& lb = inner_->block_max_distance();
-    const size_t off = static_cast<size_t>(ob0_ - lb0_) * bw_;
-    std::copy(lb.begin() + off, lb.begin() + off + rank_blocks(), mine.begin());
+// Every exchange message starts with a status word, and a rank whose local
+// step failed still takes part in the exchange: all ranks then see the
+// failure in the same collective and fail together instead of leaving the
+// others blocked in the next all-gather.
+bool StripComparator::CheckStatus(const std::vector<uint32_t>& status, const std::string& local) {
+  for (int r = 0; r < layout_.world; ++r) {
+    if (status[r] == 0) continue;
+    if (r == rank_) return Fail(local);
+    return Fail("strip comparator: rank " + std::to_string(r) + " failed");
   }
+  return true;
+}
+
+bool StripComparator::Compare(const CoeffImage& img) {
+  // message: [status][owned block maxima, padded to the largest strip]
+  std::vector<float> mine(1 + max_owned_, 0.0f);
+  uint32_t st = 0;
+  std::string local_err;
+  if (!Sync(img)) {
+    st = 1;
+    local_err = err_;
+  } else if (inner_) {
+    if (!inner_->Compare(local_)) {
+      st = 1;
+      local_err = inner_->error();
+    } else {
+      const std::vector<float>& lb = inner_->block_max_distance();
+      const size_t off = static_cast<size_t>(ob0_ - lb0_) * bw_;
+      std::copy(lb.begin() + off, lb.begin() + off + rank_blocks(), mine.begin() + 1);
+    }
+  }
+  std::memcpy(mine.data(), &st, sizeof(st));
   const auto t0 = Clock::now();
-  std::vector<float> all(static_cast<size_t>(max_owned_) * layout_.world);
+  const size_t stride = 1 + static_cast<size_t>(max_owned_);
+  std::vector<float> all(stride * layout_.world);
   if (!coll_->AllGather(mine.data(), mine.size() * sizeof(float), all.data()))
     return Fail("strip comparator: block maxima all-gather failed");
   seconds_exchange += Since(t0);
+  std::vector<uint32_t> status(layout_.world);
+  for (int r = 0; r < layout_.world; ++r) std::memcpy(&status[r], &all[r * stride], sizeof(uint32_t));
+  if (!CheckStatus(status, local_err)) return false;
   float d = 0.0f;
   for (int r = 0; r < layout_.world; ++r) {
     const int b0 = layout_.y0[r] / 8 * bw_;
     const int nb = ((layout_.y1[r] + 7) / 8 - layout_.y0[r] / 8) * bw_;
     for (int i = 0; i < nb; ++i) {
-      const float v = all[static_cast<size_t>(r) * max_owned_ + i];
+      const float v = all[static_cast<size_t>(r) * stride + 1 + i];
       block_max_[b0 + i] = v;
       d = std::max(d, v);
     }
@@ -182,7 +209,7 @@ void StripComparator::FinishBlockComparisons() {
 }
 
 bool StripComparator::BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg,
-                                         int comp_mask, int lookahead,
+                                         int comp_mask, int lookahead, bool new_model,
                                          std::vector<CoeffData>* out) {
   // The orders through the candidates' form (processor.cc:690-700 filter)
   // are all the search reads; the unfiltered form is not exchanged.
@@ -190,29 +217,38 @@ bool StripComparator::BlockZeroingOrders(const CoeffImage& img, const JpegData& 
   (void)orig_jpg;
   (void)comp_mask;
   (void)lookahead;
+  (void)new_model;
   (void)out;
   return Fail("strip comparator: use BlockZeroingCandidates");
 }
 
 bool StripComparator::BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg,
-                                             int comp_mask, int lookahead,
+                                             int comp_mask, int lookahead, bool new_model,
                                              std::vector<int>* offsets, std::vector<uint8_t>* idx,
                                              std::vector<float>* err) {
   (void)orig_jpg;
-  if (!Sync(img)) return false;
-  // this rank's owned blocks: [count per block][candidate bytes][errors]
-  std::vector<uint8_t> send;
-  if (inner_) {
-    std::vector<int> loff;
-    std::vector<uint8_t> lidx;
-    std::vector<float> lerr;
-    if (!inner_->BlockZeroingCandidates(local_, local_orig_, comp_mask, lookahead, &loff, &lidx,
-                                        &lerr))
-      return Fail(inner_->error());
+  // this rank's owned blocks: [status][count per block][candidate bytes][errors]
+  // (a failed rank sends its status alone and still takes part, see Compare)
+  std::vector<uint8_t> send(sizeof(uint32_t), 0);
+  uint32_t st = 0;
+  std::string local_err;
+  std::vector<int> loff;
+  std::vector<uint8_t> lidx;
+  std::vector<float> lerr;
+  if (!Sync(img)) {
+    st = 1;
+    local_err = err_;
+  } else if (inner_ && !inner_->BlockZeroingCandidates(local_, local_orig_, comp_mask, lookahead,
+                                                       new_model, &loff, &lidx, &lerr)) {
+    st = 1;
+    local_err = inner_->error();
+  }
+  std::memcpy(send.data(), &st, sizeof(st));
+  if (inner_ && st == 0) {
     const int b0 = (ob0_ - lb0_) * bw_, nb = rank_blocks();
     const int c0 = loff[b0], c1 = loff[b0 + nb];
-    send.resize(sizeof(int) * nb + (c1 - c0) * (1 + sizeof(float)));
-    uint8_t* p = send.data();
+    send.resize(sizeof(uint32_t) + sizeof(int) * nb + (c1 - c0) * (1 + sizeof(float)));
+    uint8_t* p = send.data() + sizeof(uint32_t);
     for (int b = 0; b < nb; ++b) {
       const int cnt = loff[b0 + b + 1] - loff[b0 + b];
       std::memcpy(p, &cnt, sizeof(int));
@@ -226,6 +262,11 @@ bool StripComparator::BlockZeroingCandidates(const CoeffImage& img, const JpegDa
   std::vector<std::vector<uint8_t>> all;
   if (!coll_->AllGatherV(send, &all)) return Fail("strip comparator: candidate all-gather failed");
   seconds_exchange += Since(t0);
+  std::vector<uint32_t> status(layout_.world, 1);
+  for (int r = 0; r < layout_.world; ++r)
+    if (all[r].size() >= sizeof(uint32_t)) std::memcpy(&status[r], all[r].data(), sizeof(uint32_t));
+  if (!CheckStatus(status, local_err)) return false;
+  for (auto& m : all) m.erase(m.begin(), m.begin() + sizeof(uint32_t));
   offsets->assign(blocks_ + 1, 0);
   idx->clear();
   err->clear();
@@ -281,17 +322,27 @@ int ProcessStrips(int device, const ProcessParams& params, const uint8_t* rgb, i
     const StripLayout L = StripLayout::Make(w, h, coll->world());
     const int r = coll->rank();
     std::unique_ptr<Comparator> inner;
+    std::string e;
     if (L.y1[r] > L.y0[r]) {
-      std::string e;
       auto c = HipButteraugliComparator::Create(device, w, L.e1[r] - L.e0[r],
                                                 rgb + static_cast<size_t>(3) * w * L.e0[r], false,
                                                 params.butteraugli_target, &e);
-      if (!c) {
-        if (err) *err = e;
-        return GZ_ERR_DEVICE;
-      }
       hip = c.get();
       inner = std::move(c);
+    }
+    // every rank reports whether its device comparator came up before any
+    // rank enters the search (a rank that returned here alone would leave the
+    // others waiting in the first exchange)
+    const uint32_t mine = (L.y1[r] > L.y0[r] && !inner) ? 1u : 0u;
+    std::vector<uint32_t> status(coll->world());
+    if (!coll->AllGather(&mine, sizeof(mine), status.data())) {
+      if (err) *err = "strip setup: status all-gather failed";
+      return GZ_ERR_INTERNAL;
+    }
+    for (int q = 0; q < coll->world(); ++q) {
+      if (status[q] == 0) continue;
+      if (err) *err = q == r ? e : "strip setup: rank " + std::to_string(q) + " failed";
+      return GZ_ERR_DEVICE;
     }
     cmp.reset(new StripComparator(L, std::move(inner), coll, params.butteraugli_target));
   }

@@ -64,9 +64,10 @@ class StripComparator : public Comparator {
   bool StartBlockComparisons() override;
   void FinishBlockComparisons() override;
   bool BlockZeroingOrders(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
-                          int lookahead, std::vector<CoeffData>* out) override;
+                          int lookahead, bool new_model, std::vector<CoeffData>* out) override;
   bool BlockZeroingCandidates(const CoeffImage& img, const JpegData& orig_jpg, int comp_mask,
-                              int lookahead, std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                              int lookahead, bool new_model, std::vector<int>* offsets,
+                              std::vector<uint8_t>* idx,
                               std::vector<float>* err) override;
   bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
                             bool need_host = true) override;
@@ -85,6 +86,8 @@ class StripComparator : public Comparator {
   double seconds_exchange = 0.0;
 
  private:
+  // Fails on every rank if any rank's status word is non-zero.
+  bool CheckStatus(const std::vector<uint32_t>& status, const std::string& local);
   bool Fail(const std::string& what);
   bool Sync(const CoeffImage& img);  // the strip's coefficients <- the whole image's
   int rank_blocks() const { return (ob1_ - ob0_) * bw_; }

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <list>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -126,6 +127,20 @@ void BuildTables(GzTables* t) {
     t->block_csf_d[i] = kBlockCsfD[i];
   }
   memcpy(t->zeroing_csf, kZeroingCsf, sizeof(kZeroingCsf));
+  {
+    static const uint8_t kZigZag[64] = {
+        0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+        3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+        10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+        21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+    static const uint8_t kOldCsf[64] = {
+        10, 10, 20, 40, 60, 70, 80, 90, 10, 20, 30, 60, 70, 80, 90, 90,
+        20, 30, 60, 70, 80, 90, 90, 90, 40, 60, 70, 80, 90, 90, 90, 90,
+        60, 70, 80, 90, 90, 90, 90, 90, 70, 80, 90, 90, 90, 90, 90, 90,
+        80, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90};
+    memcpy(t->zigzag, kZigZag, sizeof(kZigZag));
+    memcpy(t->old_csf, kOldCsf, sizeof(kOldCsf));
+  }
   memcpy(t->idct, kIdct, sizeof(kIdct));
   BuildBlur(1.1f, 0.0f, &t->blur[kSigOpsin]);
   BuildBlur(1.5f, 0.0f, &t->blur[kSigEdgeX]);
@@ -334,6 +349,7 @@ bool Engine::Fail(const char* what, int code) {
   snprintf(buf, sizeof(buf), "%s failed: %s (%d)", what,
            hipGetErrorString(static_cast<hipError_t>(code)), code);
   err_ = buf;
+  failed_ = true;
   return false;
 }
 
@@ -384,6 +400,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   bool ok = true;
   auto alloc = [&](void** p, size_t bytes) {
     if (ok && hipMalloc(p, bytes) != hipSuccess) ok = false;
+    e->bytes_ += bytes;
   };
   alloc(reinterpret_cast<void**>(&e->d_rgb_), 3 * n);
   alloc(reinterpret_cast<void**>(&e->d_orig_), nc * sizeof(int16_t));
@@ -437,6 +454,8 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
     ok = false;
   if (!ok) return fail("device allocation failed");
+  // pinned staging (coefficients, offsets, histograms, block maxima)
+  e->bytes_ += nc * sizeof(int16_t) + static_cast<size_t>(e->nb_) * 12 + 8192;
   k_blur_scales<<<dim3((e->scale_stride_ + 255) / 256, kNumSigmas * 2), 256, 0, s>>>(
       w, h, e->scale_stride_, e->d_scales_);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
@@ -446,30 +465,84 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
 
 namespace {
 std::mutex g_pool_mu;
-// Intentionally leaked: idle engines must not be freed from a static
-// destructor after the HIP runtime has shut down.
-auto* g_pool = new std::map<std::tuple<int, int, int>, std::vector<std::unique_ptr<Engine>>>;
+// Idle engines, most recently released first.  Intentionally leaked: idle
+// engines must not be freed from a static destructor after the HIP runtime
+// has shut down.
+auto* g_idle = new std::list<std::unique_ptr<Engine>>;
+size_t g_idle_bytes = 0;
 constexpr size_t kMaxIdlePerKey = 8;
+
+size_t PoolCapBytes() {
+  static const size_t cap = [] {
+    const char* v = getenv("GZ_ENGINE_POOL_BYTES");
+    return v ? static_cast<size_t>(strtoull(v, nullptr, 10)) : (static_cast<size_t>(16) << 30);
+  }();
+  return cap;
+}
+
+// Unlinks least recently used engines until the idle set is within
+// keep_bytes and every size has at most kMaxIdlePerKey; the caller destroys
+// them outside the lock.  g_pool_mu held.
+void EvictLocked(size_t keep_bytes, std::vector<std::unique_ptr<Engine>>* out) {
+  std::map<std::tuple<int, int, int>, size_t> per_key;
+  for (auto it = g_idle->begin(); it != g_idle->end();) {
+    size_t& n = per_key[std::make_tuple((*it)->device(), (*it)->width(), (*it)->height())];
+    if (++n > kMaxIdlePerKey) {
+      g_idle_bytes -= (*it)->bytes();
+      out->push_back(std::move(*it));
+      it = g_idle->erase(it);
+    } else {
+      ++it;
+    }
+  }
+  while (g_idle_bytes > keep_bytes && !g_idle->empty()) {
+    g_idle_bytes -= g_idle->back()->bytes();
+    out->push_back(std::move(g_idle->back()));
+    g_idle->pop_back();
+  }
+}
 }  // namespace
 
 std::unique_ptr<Engine> AcquireEngine(int device, int w, int h, std::string* err) {
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    auto it = g_pool->find(std::make_tuple(device, w, h));
-    if (it != g_pool->end() && !it->second.empty()) {
-      std::unique_ptr<Engine> e = std::move(it->second.back());
-      it->second.pop_back();
-      return e;
+    for (auto it = g_idle->begin(); it != g_idle->end(); ++it) {
+      if ((*it)->device() == device && (*it)->width() == w && (*it)->height() == h) {
+        std::unique_ptr<Engine> e = std::move(*it);
+        g_idle->erase(it);
+        g_idle_bytes -= e->bytes();
+        return e;
+      }
     }
   }
   return Engine::Create(device, w, h, err);
 }
 
 void ReleaseEngine(std::unique_ptr<Engine> e) {
-  if (!e) return;
+  if (!e || e->failed()) return;  // a failed engine is destroyed, never reused
+  std::vector<std::unique_ptr<Engine>> evicted;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_idle_bytes += e->bytes();
+    g_idle->push_front(std::move(e));
+    EvictLocked(PoolCapBytes(), &evicted);
+  }
+}
+
+size_t TrimEnginePool(size_t keep_bytes) {
+  std::vector<std::unique_ptr<Engine>> evicted;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    EvictLocked(keep_bytes, &evicted);
+  }
+  size_t freed = 0;
+  for (const auto& e : evicted) freed += e->bytes();
+  return freed;
+}
+
+size_t EnginePoolIdleBytes() {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  auto& v = (*g_pool)[std::make_tuple(e->device(), e->width(), e->height())];
-  if (v.size() < kMaxIdlePerKey) v.push_back(std::move(e));
+  return g_idle_bytes;
 }
 
 Engine::~Engine() {
@@ -822,7 +895,8 @@ bool Engine::OrderBlocks(int comp_mask) {
   return true;
 }
 
-bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out) {
+bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool new_model,
+                                CoeffDataHost* out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   unsigned long long* timers = nullptr;
@@ -835,7 +909,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
-                                     comp_mask, limit, lookahead,
+                                     comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
@@ -854,7 +928,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, Coeff
   return true;
 }
 
-bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
+bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, bool new_model,
                                     std::vector<int>* offsets, std::vector<uint8_t>* idx,
                                     std::vector<float>* err) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
@@ -862,7 +936,7 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead,
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
-                                     comp_mask, limit, lookahead,
+                                     comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
   if (!ScanCounts(d_zero_count_, nb_, d_zero_off_, "scan_counts")) return false;
   GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 3) / 4, 256, 0, s>>>(

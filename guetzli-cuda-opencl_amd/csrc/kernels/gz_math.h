@@ -90,6 +90,8 @@ struct GzTables {
   float block_csf[37];                             // :103-144
   double block_csf_d[37];                          // butteraugli.cc:157-198
   float zeroing_csf[192];                          // order.inc:3
+  uint8_t zigzag[64];                              // kJPEGZigZagOrder, jpeg_data.h:73-82
+  uint8_t old_csf[64];                             // oldCsf, processor.cc:381-390
   int idct[64];                                    // idct.cc:29-38
   float opsin8_scale[8];  // border scales of the sigma-1.1 blur on an 8-wide axis (8x8 opsin)
   BlurSpec blur[kNumSigmas];
@@ -271,19 +273,6 @@ __device__ __forceinline__ void opsin_absorbance(float r, float g, float b, floa
   out[2] = 0.0882062883536f * r + 0.158581714673f * g + 0.712857943858f * b + 10.6524069248f;
 }
 
-__device__ __forceinline__ float clenshaw6(float x, float c0, float c1, float c2, float c3,
-                                           float c4, float c5) {
-  // ClenshawRecursionOpt<5..0>, :806-824
-  float b1 = 0.0f, b2 = 0.0f, xb, t;
-  xb = x * b1; t = (xb + xb) - b2 + c5; b2 = b1; b1 = t;
-  xb = x * b1; t = (xb + xb) - b2 + c4; b2 = b1; b1 = t;
-  xb = x * b1; t = (xb + xb) - b2 + c3; b2 = b1; b1 = t;
-  xb = x * b1; t = (xb + xb) - b2 + c2; b2 = b1; b1 = t;
-  xb = x * b1; t = (xb + xb) - b2 + c1; b2 = b1; b1 = t;
-  xb = x * b1;
-  return xb - b2 + c0;
-}
-
 __device__ __forceinline__ f32x2 clenshaw6x2(float x, f32x2 c0, f32x2 c1, f32x2 c2, f32x2 c3,
                                              f32x2 c4, f32x2 c5) {
   const f32x2 xx = {x, x};
@@ -341,7 +330,7 @@ __device__ __forceinline__ float gamma_poly(float x) {
   // where both forms give -1.0f
   const float xc = 2.0f * x01 - 1.0f;
   // numerator and denominator recursions side by side in packed f32 (each
-  // half is clenshaw6's exact operation sequence)
+  // half is ClenshawRecursionOpt's exact operation sequence, :806-824)
   const f32x2 r = clenshaw6x2(xc, f32x2{881.979476556478289f, 12.262350348616792f},
                               f32x2{1496.058452015812463f, 20.557285797683576f},
                               f32x2{908.662212739659481f, 12.161463238367844f},

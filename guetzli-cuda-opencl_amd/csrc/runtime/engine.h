@@ -56,6 +56,10 @@ class Engine {
   int device() const { return device_; }
   int width() const { return w_; }
   int height() const { return h_; }
+  // HBM + pinned host bytes held (the pool's accounting unit).
+  size_t bytes() const { return bytes_; }
+  // An operation on this engine failed: it is not returned to the pool.
+  bool failed() const { return failed_; }
   int blocks() const { return nb_; }
 
   // Reference image (RGB8 interleaved); computes and caches its XYB.
@@ -81,12 +85,16 @@ class Engine {
   // Mask(ref, ref) sampled at block corners (StartBlockComparisons).
   bool StartBlockComparisons(float* mask_scale_host /* 3*blocks, may be null */);
   // Per-block greedy zeroing orders for the current candidate.
-  bool BlockZeroingOrders(int comp_mask, float limit, int lookahead, CoeffDataHost* out);
+  // new_model: Params::new_zeroing_model (false: the old candidate key,
+  // processor.cc:400-405).
+  bool BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool new_model,
+                          CoeffDataHost* out);
   // The same search, reduced on the device to what the back end consumes:
   // per block the entries with 0 < block_err <= limit, in order, concatenated
   // (offsets: blocks + 1 entries).  Moves ~5 B per kept entry instead of the
   // 1.5 KB-per-block order table.
-  bool BlockZeroingCandidates(int comp_mask, float limit, int lookahead, std::vector<int>* offsets,
+  bool BlockZeroingCandidates(int comp_mask, float limit, int lookahead, bool new_model,
+                              std::vector<int>* offsets,
                               std::vector<uint8_t>* idx, std::vector<float>* err);
 
   // Device entropy coding of the current coefficients with quant q (the
@@ -131,6 +139,8 @@ class Engine {
   size_t n_ = 0;
   void* stream_ = nullptr;
   std::string err_;
+  bool failed_ = false;
+  size_t bytes_ = 0;
   bool have_mask_scale_ = false;
 
   // device buffers
@@ -195,9 +205,16 @@ class Engine {
 
 // Process-wide pool of idle engines keyed by (device, width, height): an
 // encode reuses the HBM buffers, stream and tables of an earlier encode of
-// the same size instead of re-allocating ~40 planes.
+// the same size instead of re-allocating ~40 planes.  Idle engines are kept
+// in least-recently-released order under a byte cap (GZ_ENGINE_POOL_BYTES,
+// default 16 GiB of HBM + pinned memory, and at most 8 per size); an engine
+// whose last operation failed is destroyed instead of pooled.
 std::unique_ptr<Engine> AcquireEngine(int device, int w, int h, std::string* err);
 void ReleaseEngine(std::unique_ptr<Engine> e);
+// Destroys least recently used idle engines until at most keep_bytes stay
+// pooled; returns the bytes released.
+size_t TrimEnginePool(size_t keep_bytes);
+size_t EnginePoolIdleBytes();
 
 // Per-launch HIP-event timing (off by default).
 void ProfileEnable(bool on);

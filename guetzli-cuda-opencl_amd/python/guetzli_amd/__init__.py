@@ -24,6 +24,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))
 LIB_PATH = os.environ.get("GZ_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libguetzli_hip.so")
 
 GZ_OK = 0
+GZ_ERR_INVALID_ARG, GZ_ERR_DEVICE, GZ_ERR_OUT_OF_MEMORY, GZ_ERR_UNSUPPORTED, GZ_ERR_INTERNAL = 1, 2, 3, 4, 5
 _STATUS = {1: "invalid argument", 2: "device error", 3: "out of memory", 4: "unsupported",
            5: "internal error"}
 
@@ -72,6 +73,7 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
+    "gz_block_error_adjustment_weights", "gz_engine_pool_trim", "gz_engine_pool_idle_bytes",
     "gz_comparator_original_coeffs", "gz_comparator_write_jpeg", "gz_write_jpeg_host",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
@@ -134,8 +136,15 @@ def lib():
     L.gz_comparator_score_output_size.restype = ctypes.c_double
     L.gz_comparator_start_block_comparisons.argtypes = [vp, vp]
     L.gz_comparator_start_block_comparisons.restype = i32
-    L.gz_comparator_block_zeroing_orders.argtypes = [vp, vp, vp, i32, f32, i32, vp]
+    L.gz_comparator_block_zeroing_orders.argtypes = [vp, vp, vp, i32, f32, i32, i32, vp]
     L.gz_comparator_block_zeroing_orders.restype = i32
+    L.gz_block_error_adjustment_weights.argtypes = [i32, i32, f32, i32, i32, ctypes.c_double, i32,
+                                                    i32, vp, vp]
+    L.gz_block_error_adjustment_weights.restype = i32
+    L.gz_engine_pool_trim.argtypes = [ctypes.c_size_t]
+    L.gz_engine_pool_trim.restype = ctypes.c_size_t
+    L.gz_engine_pool_idle_bytes.argtypes = []
+    L.gz_engine_pool_idle_bytes.restype = ctypes.c_size_t
     L.gz_comparator_original_coeffs.argtypes = [vp, vp]
     L.gz_comparator_original_coeffs.restype = i32
     L.gz_comparator_write_jpeg.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_void_p),
@@ -466,6 +475,32 @@ def rgb_to_coeffs(rgb, width, height):
     return out
 
 
+def engine_pool_trim(keep_bytes=0):
+    """Destroys idle pooled engines until at most keep_bytes remain."""
+    return int(lib().gz_engine_pool_trim(keep_bytes))
+
+
+def engine_pool_idle_bytes():
+    return int(lib().gz_engine_pool_idle_bytes())
+
+
+def block_error_adjustment_weights(width, height, target, direction, max_block_dist, distmap,
+                                   target_mul=1.0, factor_x=1, factor_y=1, block_weight=None):
+    """ComputeBlockErrorAdjustmentWeights (butteraugli_comparator.cc:169-233)
+    on the host; block_weight (zeros by default) is updated and returned."""
+    d = np.ascontiguousarray(distmap, dtype=np.float32).reshape(-1)
+    if d.size != width * height:
+        raise ValueError("distmap must hold width*height floats")
+    nb = ((width + 8 * factor_x - 1) // (8 * factor_x)) * ((height + 8 * factor_y - 1) // (8 * factor_y))
+    wgt = np.zeros(nb, np.float32) if block_weight is None else \
+        np.ascontiguousarray(block_weight, dtype=np.float32).copy()
+    _check(lib().gz_block_error_adjustment_weights(width, height, ctypes.c_float(target), direction,
+                                                   max_block_dist, target_mul, factor_x, factor_y,
+                                                   _ptr(d), _ptr(wgt)),
+           "block_error_adjustment_weights")
+    return wgt
+
+
 class ButteraugliComparator:
     """guetzli::ButteraugliComparator (butteraugli_comparator.h:33-81) on the GPU."""
 
@@ -554,10 +589,13 @@ class ButteraugliComparator:
                "original_coeffs")
         return out
 
-    def block_zeroing_orders(self, cur_coeffs, orig_coeffs, limit, comp_mask=7, lookahead=3):
+    def block_zeroing_orders(self, cur_coeffs, orig_coeffs, limit, comp_mask=7, lookahead=3,
+                             new_zeroing_model=True):
+        """Per-block greedy zeroing orders (processor.cc:376-487), blocks x 192."""
         out = np.zeros(self.blocks * 192, dtype=COEFF_DTYPE)
         _check(lib().gz_comparator_block_zeroing_orders(
             self._h, _ptr(self._coeffs(cur_coeffs)), _ptr(self._coeffs(orig_coeffs)), comp_mask,
-            ctypes.c_float(limit), lookahead, ctypes.c_void_p(out.ctypes.data)),
+            ctypes.c_float(limit), lookahead, 1 if new_zeroing_model else 0,
+            ctypes.c_void_p(out.ctypes.data)),
             "block_zeroing_orders")
         return out.reshape(self.blocks, 192)

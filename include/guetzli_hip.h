@@ -174,6 +174,15 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
 gz_status gz_comparator_original_coeffs(gz_comparator* cmp, int16_t* out);
 /* Per-8x8-block maxima of the last distance map (ceil(w/8)*ceil(h/8)). */
 gz_status gz_comparator_block_max(gz_comparator* cmp, float* out);
+/* ComputeBlockErrorAdjustmentWeights (butteraugli_comparator.cc:169-233) on
+ * the host: per-(8*factor)-block maxima of `distmap` (width*height floats),
+ * then the neighbourhood weights.  block_weight (one float per block) is
+ * updated in place -- the caller zero-fills it first, as the search loop does
+ * (processor.cc:779-783).  No device needed. */
+gz_status gz_block_error_adjustment_weights(int width, int height, float target, int direction,
+                                            int max_block_dist, double target_mul, int factor_x,
+                                            int factor_y, const float* distmap,
+                                            float* block_weight);
 /* Comparator::DistanceOK (butteraugli_comparator.h:52-54). */
 int gz_comparator_distance_ok(gz_comparator* cmp, double target_mul);
 /* Comparator::ScoreOutputSize (butteraugli_comparator.cc:235-237). */
@@ -185,10 +194,14 @@ gz_status gz_comparator_start_block_comparisons(gz_comparator* cmp, float* mask_
  * (processor.cc:376-487, 641-672) for the candidate `cur_coeffs` against
  * the original q=1 coefficients `orig_coeffs`; out: blocks*192 entries,
  * zero-filled tails.  Replaces cuComputeBlockZeroingOrder
- * (clguetzli/cuguetzli.h:30-40). */
+ * (clguetzli/cuguetzli.h:30-40).  comp_mask: components searched (the
+ * others keep cur_coeffs' values in the pixels); lookahead /
+ * new_zeroing_model: Params::zeroing_greedy_lookahead / new_zeroing_model
+ * (0: the old candidate key of processor.cc:400-405). */
 gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* cur_coeffs,
                                              const int16_t* orig_coeffs, int comp_mask,
-                                             float limit, int lookahead, gz_coeff_data* out);
+                                             float limit, int lookahead, int new_zeroing_model,
+                                             gz_coeff_data* out);
 
 /* SaveToJpegData + WriteJpeg (guetzli/output_image.cc:579-640,
  * jpeg_data_writer.cc:540-553) of dequantized coefficients `coeffs`
@@ -200,6 +213,15 @@ gz_status gz_comparator_write_jpeg(gz_comparator* cmp, const int16_t* coeffs, co
 /* The same on the host (the library's serial writer; no device needed). */
 gz_status gz_write_jpeg_host(int width, int height, const int16_t* coeffs, const int* quant,
                              uint8_t** jpeg_out, size_t* jpeg_size);
+
+/* ---- device memory ---------------------------------------------------- */
+/* Encodes keep their per-size engines (HBM buffers, stream, graph) in a
+ * process-wide pool for reuse: least recently used first out, capped at
+ * GZ_ENGINE_POOL_BYTES (environment, default 16 GiB) and 8 per image size;
+ * engines whose last operation failed are never pooled.  trim destroys idle
+ * engines until at most keep_bytes remain and returns the bytes released. */
+size_t gz_engine_pool_trim(size_t keep_bytes);
+size_t gz_engine_pool_idle_bytes(void);
 
 /* ---- measurement ------------------------------------------------------ */
 /* Per-launch timing with HIP events on each object's own stream (off by

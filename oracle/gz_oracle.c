@@ -1182,7 +1182,21 @@ static double compare_block(const float* rgb0_c, const float* cand_lin, const fl
 
 void gzo_block_zeroing_orders(int w, int h, const uint8_t* ref_rgb, const float* ref_mask,
                               const int16_t* cur_coeffs, const int16_t* orig_coeffs,
-                              float limit, int lookahead, gzo_coeff_data* out) {
+                              float limit, int lookahead, int comp_mask, int new_model,
+                              gzo_coeff_data* out) {
+  /* old zeroing model (processor.cc:381-405) */
+  static const uint8_t kOldCsf[64] = {
+      10, 10, 20, 40, 60, 70, 80, 90, 10, 20, 30, 60, 70, 80, 90, 90,
+      20, 30, 60, 70, 80, 90, 90, 90, 40, 60, 70, 80, 90, 90, 90, 90,
+      60, 70, 80, 90, 90, 90, 90, 90, 70, 80, 90, 90, 90, 90, 90, 90,
+      80, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90, 90};
+  static const double kWeight[3] = {1.0, 0.22, 0.20};
+  /* kJPEGZigZagOrder, jpeg_data.h:73-82: zigzag position of natural index k */
+  static const int kZigZagOrder[64] = {
+      0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+      3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+      10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+      21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
   gzo_init();
   const int bw = (w + 7) / 8, bh = (h + 7) / 8;
   const size_t nb = (size_t)bw * bh, n = (size_t)w * h;
@@ -1197,15 +1211,23 @@ void gzo_block_zeroing_orders(int w, int h, const uint8_t* ref_rgb, const float*
       int idxs[192];
       float keys[192];
       int ncand = 0;
-      for (int c = 0; c < 3; ++c)
+      /* SelectFrequencyMasking passes only the masked components
+       * (processor.cc:645-655); the image keeps the others' current values */
+      for (int c = 0; c < 3; ++c) {
+        if (!(comp_mask & (1 << c))) continue;
         for (int k = 1; k < 64; ++k) {
           const int idx = c * 64 + k;
           if (block[idx] != 0) {
             idxs[ncand] = idx;
-            keys[ncand] = abs(orig[idx]) * kZeroingCsf[idx] + 0.0f;
+            if (new_model)
+              keys[ncand] = abs(orig[idx]) * kZeroingCsf[idx] + 0.0f;
+            else
+              keys[ncand] = (float)((abs(orig[idx]) - kZigZagOrder[k] / 64.0) * kWeight[c] /
+                                    kOldCsf[k]);
             ++ncand;
           }
         }
+      }
       gzo_sort_pairs(idxs, keys, ncand);
       /* SwitchBlock: 8x8-local opsin of the original block */
       float rgb0_c[192];

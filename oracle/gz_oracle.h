@@ -89,10 +89,13 @@ void gzo_sort_pairs(int* idx, float* key, int n);
 /* Per-block greedy zeroing order of the CPU_OPT loop
  * (processor.cc:376-487, 641-672; butteraugli_comparator.cc:72-163).
  * ref_mask: MaskOpt(ref_xyb, ref_xyb).mask (3*w*h), i.e. mask_xyz_.
+ * comp_mask: components searched (others keep cur's values); new_model:
+ * Params::new_zeroing_model (false: the oldCsf / kWeight key, :400-405).
  * out: blocks*192 entries, zero-filled tails. */
 void gzo_block_zeroing_orders(int w, int h, const uint8_t* ref_rgb, const float* ref_mask,
                               const int16_t* cur_coeffs, const int16_t* orig_coeffs,
-                              float limit, int lookahead, gzo_coeff_data* out);
+                              float limit, int lookahead, int comp_mask, int new_model,
+                              gzo_coeff_data* out);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,8 @@
 // restatement (oracle/gz_oracle.c) and the HIP product are pinned against.
 //
 //   guetzli_ref encode  RGB W H QUALITY OUT.jpg [c|cpu]     guetzli.cc:247-368
-//   guetzli_ref stages  RGB W H QSEED OUTDIR                 see dump_stages()
+//   guetzli_ref stages  RGB W H QSEED OUTDIR                 see Stages()
+//   guetzli_ref zero_variants RGB W H QSEED OUTDIR           see ZeroVariants()
 //   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg            processor.cc:1029-1066
 //   guetzli_ref decode  IN.jpg OUT.rgb OUT.coeffs             ReadJpeg + DecodeJpegToRGB
 //
@@ -159,6 +160,86 @@ void MakeQ(int seed, int q[3][64]) {
     }
 }
 
+// Per-block greedy zeroing orders of every block (the CPU_OPT loop of
+// SelectFrequencyMasking, processor.cc:641-672, factor 1) for the given
+// Params::zeroing_greedy_lookahead / new_zeroing_model and comp_mask.  As in
+// SelectFrequencyMasking, only the masked components of the current and
+// original blocks are passed (ComputeBlockZeroingOrder's REQUIRES, :374);
+// the image keeps every component's current coefficients.
+std::vector<guetzli::CoeffData> ZeroOrders(const std::vector<uint8_t>& rgb, int w, int h,
+                                           float target, const guetzli::JPEGData& jpg,
+                                           guetzli::OutputImage* img, int lookahead,
+                                           int comp_mask, bool new_model) {
+  guetzli::ProcessStats stats;
+  guetzli::Processor proc;
+  guetzli::Params params;
+  params.butteraugli_target = target;
+  params.zeroing_greedy_lookahead = lookahead;
+  params.new_zeroing_model = new_model;
+  guetzli::ButteraugliComparator c3(w, h, &rgb, target, &stats);
+  proc.params_ = params;
+  proc.comparator_ = &c3;
+  proc.stats_ = &stats;
+  c3.StartBlockComparisons();
+  const int bw = (w + 7) / 8, bh = (h + 7) / 8;
+  std::vector<guetzli::CoeffData> out(bw * bh * 192);
+  memset(out.data(), 0, out.size() * sizeof(out[0]));
+  for (int by = 0, bix = 0; by < bh; ++by)
+    for (int bx = 0; bx < bw; ++bx, ++bix) {
+      guetzli::coeff_t block[192] = {0}, orig_block[192] = {0};
+      for (int c = 0; c < 3; ++c) {
+        if (!(comp_mask & (1 << c))) continue;
+        img->component(c).GetCoeffBlock(bx, by, &block[c * 64]);
+        const auto& comp = jpg.components[c];
+        memcpy(&orig_block[c * 64], &comp.coeffs[(by * comp.width_in_blocks + bx) * 64],
+               64 * sizeof(guetzli::coeff_t));
+      }
+      std::vector<guetzli::CoeffData> order;
+      proc.ComputeBlockZeroingOrder(block, orig_block, bx, by, 1, 1,
+                                    static_cast<uint8_t>(comp_mask), img, &order);
+      for (size_t i = 0; i < order.size(); ++i) out[bix * 192 + i] = order[i];
+    }
+  c3.FinishBlockComparisons();
+  return out;
+}
+
+// Candidate image of the stage fixtures: EncodeRGBToJpeg -> remove quant ->
+// copy -> global quantization (processor.cc:1160-1163, 94-107, 310-317).
+bool StageCandidate(const std::vector<uint8_t>& rgb, int w, int h, int qseed,
+                    guetzli::JPEGData* jpg, guetzli::OutputImage* img, int q[3][64]) {
+  if (!guetzli::EncodeRGBToJpeg(rgb, w, h, jpg)) return false;
+  int q_in[3][64];
+  guetzli::RemoveOriginalQuantization(jpg, q_in);
+  MakeQ(qseed, q);
+  img->CopyFromJpegData(*jpg);
+  img->ApplyGlobalQuantization(q);
+  return true;
+}
+
+// Zeroing-order variants of a stage fixture: lookahead 1 and 2, comp_mask 1
+// (Y only) and 6 (Cb+Cr), and the old zeroing model (new_zeroing_model =
+// false, processor.cc:400-405) -> OUTDIR/zero_order_la<L>_m<M>_nm<N>.bin.
+int ZeroVariants(int argc, char** argv) {
+  if (argc < 7) return 1;
+  std::vector<uint8_t> rgb = ReadAll(argv[2]);
+  const int w = atoi(argv[3]), h = atoi(argv[4]), qseed = atoi(argv[5]);
+  const std::string dir = argv[6];
+  g_mathMode = MODE_CPU_OPT;
+  const float target = static_cast<float>(guetzli::ButteraugliScoreForQuality(95));
+  guetzli::JPEGData jpg;
+  guetzli::OutputImage img(w, h);
+  int q[3][64];
+  if (!StageCandidate(rgb, w, h, qseed, &jpg, &img, q)) return 4;
+  static const int kVariants[][3] = {{1, 7, 1}, {2, 7, 1}, {3, 1, 1}, {3, 6, 1}, {3, 7, 0}, {2, 6, 0}};
+  for (const auto& v : kVariants) {
+    std::vector<guetzli::CoeffData> out = ZeroOrders(rgb, w, h, target, jpg, &img, v[0], v[1], v[2] != 0);
+    char name[96];
+    snprintf(name, sizeof(name), "/zero_order_la%d_m%d_nm%d.bin", v[0], v[1], v[2]);
+    WriteAll(dir + name, out.data(), out.size() * sizeof(out[0]));
+  }
+  return 0;
+}
+
 int Stages(int argc, char** argv) {
   if (argc < 7) return 1;
   std::vector<uint8_t> rgb = ReadAll(argv[2]);
@@ -269,31 +350,7 @@ int Stages(int argc, char** argv) {
   // Per-block greedy zeroing order, CPU_OPT loop of SelectFrequencyMasking
   // (processor.cc:641-672) with comp_mask 7, factor 1.
   {
-    guetzli::Processor proc;
-    guetzli::Params params;
-    params.butteraugli_target = target;
-    guetzli::ButteraugliComparator c3(w, h, &rgb, target, &stats);
-    proc.params_ = params;
-    proc.comparator_ = &c3;
-    proc.stats_ = &stats;
-    c3.StartBlockComparisons();
-    const int bw = (w + 7) / 8, bh = (h + 7) / 8;
-    std::vector<guetzli::CoeffData> out(bw * bh * 192);
-    memset(out.data(), 0, out.size() * sizeof(out[0]));
-    for (int by = 0, bix = 0; by < bh; ++by)
-      for (int bx = 0; bx < bw; ++bx, ++bix) {
-        guetzli::coeff_t block[192] = {0}, orig_block[192] = {0};
-        for (int c = 0; c < 3; ++c) {
-          img.component(c).GetCoeffBlock(bx, by, &block[c * 64]);
-          const auto& comp = jpg.components[c];
-          memcpy(&orig_block[c * 64], &comp.coeffs[(by * comp.width_in_blocks + bx) * 64],
-                 64 * sizeof(guetzli::coeff_t));
-        }
-        std::vector<guetzli::CoeffData> order;
-        proc.ComputeBlockZeroingOrder(block, orig_block, bx, by, 1, 1, 7, &img, &order);
-        for (size_t i = 0; i < order.size(); ++i) out[bix * 192 + i] = order[i];
-      }
-    c3.FinishBlockComparisons();
+    std::vector<guetzli::CoeffData> out = ZeroOrders(rgb, w, h, target, jpg, &img, 3, 7, true);
     WriteAll(dir + "/zero_order.bin", out.data(), out.size() * sizeof(out[0]));
   }
   fclose(meta);
@@ -305,6 +362,7 @@ int Stages(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "encode")) return Encode(argc, argv);
   if (argc >= 2 && !strcmp(argv[1], "stages")) return Stages(argc, argv);
+  if (argc >= 2 && !strcmp(argv[1], "zero_variants")) return ZeroVariants(argc, argv);
   if (argc >= 2 && !strcmp(argv[1], "encode_jpeg")) return EncodeJpeg(argc, argv);
   if (argc >= 2 && !strcmp(argv[1], "decode")) return Decode(argc, argv);
   fprintf(stderr,

@@ -10,7 +10,8 @@ except those files.
                    image (oracle/ref_driver.cc `stages`): reference/candidate
                    XYB, MHIC planes, edge / block-diff / low-freq / mask /
                    combined maps, distmap, block weights, per-block zeroing
-                   orders.
+                   orders (+ zero_order_la*_m*_nm*.bin: lookahead / comp_mask /
+                   zeroing-model variants).
   manifest.json    end-to-end known answers: sha256 / size / iterations of
                    `guetzli --c` on bees.png and on synthetic frames.
 """
@@ -88,6 +89,18 @@ def run_stages():
         print("stages", name, w, h)
 
 
+def run_zero_variants():
+    """zero_order_la<L>_m<M>_nm<N>.bin next to each stage fixture: the
+    per-block zeroing orders for lookahead 1/2, comp_mask 1/6 and the old
+    zeroing model (oracle/ref_driver.cc ZeroVariants)."""
+    for name, _, qseed in STAGE_CASES:
+        d = os.path.join(HERE, "stages_" + name)
+        meta = dict(l.split() for l in open(os.path.join(d, "meta.txt")) if len(l.split()) == 2)
+        subprocess.run([REF, "zero_variants", os.path.join(d, "input.rgb"), meta["w"], meta["h"],
+                        str(qseed), d], check=True)
+        print("zero variants", name)
+
+
 def run_e2e(manifest, cases):
     out = manifest.setdefault("e2e", {})
     for name, rgb, w, h, q in cases:
@@ -107,6 +120,8 @@ def main():
     what = sys.argv[1:] or ["stages", "e2e-small"]
     if "stages" in what:
         run_stages()
+    if "stages" in what or "zero-variants" in what:
+        run_zero_variants()
     if "e2e-small" in what:
         cases = [("bees_q95", os.path.join(HERE, "bees.rgb"), 444, 258, 95)]
         for name, _, _ in STAGE_CASES:

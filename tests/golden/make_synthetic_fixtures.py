@@ -5,6 +5,7 @@ Build container only; writes tests/golden/manifest.json["synthetic"].
 
   python tests/golden/make_synthetic_fixtures.py [name ...]
 """
+import fcntl
 import hashlib
 import json
 import os
@@ -23,6 +24,15 @@ CASES = {
     "synth_1920x1080_s0_q95": (0, 1920, 1080, 95),
     "synth_1920x1080_s1_q95": (1, 1920, 1080, 95),
     "synth_3840x2160_s0_q90": (0, 3840, 2160, 90),
+    # bench.py verifies every timed frame (seeds 0..7 at 1080p q95)
+    "synth_1920x1080_s2_q95": (2, 1920, 1080, 95),
+    "synth_1920x1080_s3_q95": (3, 1920, 1080, 95),
+    "synth_1920x1080_s4_q95": (4, 1920, 1080, 95),
+    "synth_1920x1080_s5_q95": (5, 1920, 1080, 95),
+    "synth_1920x1080_s6_q95": (6, 1920, 1080, 95),
+    "synth_1920x1080_s7_q95": (7, 1920, 1080, 95),
+    # configs[4]: ~35 min of reference CPU time, ~7 GB host memory
+    "synth_8192x8192_s0_q84": (0, 8192, 8192, 84),
 }
 
 
@@ -38,13 +48,19 @@ def main():
         res = subprocess.run([REF, "encode", inp, str(w), str(h), str(q), jpg, "c"], check=True,
                              capture_output=True, text=True)
         info = json.loads(res.stdout)
-        manifest = json.load(open(path))
-        manifest.setdefault("synthetic", {})[name] = {
+        entry = {
             "seed": seed, "w": w, "h": h, "quality": q,
             "input_sha256": hashlib.sha256(rgb).hexdigest(),
             "sha256": hashlib.sha256(open(jpg, "rb").read()).hexdigest(),
             "bytes": info["bytes"], "iters": info["iters"], "ref_seconds": info["seconds"]}
-        json.dump(manifest, open(path, "w"), indent=1, sort_keys=True)
+        os.unlink(inp)
+        # several generators may run concurrently: read-modify-write under a lock
+        with open(path + ".lock", "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            manifest = json.load(open(path))
+            manifest.setdefault("synthetic", {})[name] = entry
+            json.dump(manifest, open(path, "w"), indent=1, sort_keys=True)
+        manifest["synthetic"][name] = entry
         print(name, manifest["synthetic"][name], flush=True)
 
 

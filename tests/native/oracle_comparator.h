@@ -23,7 +23,15 @@ class OracleComparator : public gz::Comparator {
     bh_ = (h + 7) / 8;
     block_max_.assign(bw_ * bh_, 0.0f);
   }
+  // Failure injection (strip tests): the n-th Compare / BlockZeroingOrders
+  // call (1-based) fails; -1: never.
+  int fail_compare_at = -1, fail_zeroing_at = -1;
+
   bool Compare(const gz::CoeffImage& img) override {
+    if (++n_compare_ == fail_compare_at) {
+      err_ = "injected Compare failure";
+      return false;
+    }
     std::vector<float> dm(static_cast<size_t>(w_) * h_);
     distance_ = gzo_compare(w_, h_, rgb_.data(), img.coeffs.data(), dm.data());
     for (int by = 0; by < bh_; ++by)
@@ -46,11 +54,15 @@ class OracleComparator : public gz::Comparator {
   }
   void FinishBlockComparisons() override { mask_.clear(); }
   bool BlockZeroingOrders(const gz::CoeffImage& img, const gz::JpegData&, int comp_mask,
-                          int lookahead, std::vector<gz::CoeffData>* out) override {
-    if (comp_mask != 7) return false;
+                          int lookahead, bool new_model, std::vector<gz::CoeffData>* out) override {
+    if (++n_zeroing_ == fail_zeroing_at) {
+      err_ = "injected zeroing failure";
+      return false;
+    }
     out->resize(static_cast<size_t>(img.blocks) * 192);
     gzo_block_zeroing_orders(w_, h_, rgb_.data(), mask_.data(), img.coeffs.data(), orig_.data(),
-                             target_, lookahead, reinterpret_cast<gzo_coeff_data*>(out->data()));
+                             target_, lookahead, comp_mask, new_model ? 1 : 0,
+                             reinterpret_cast<gzo_coeff_data*>(out->data()));
     return true;
   }
   bool QuantizeFromOriginal(const int q[3][64], gz::CoeffImage* img, bool) override {
@@ -80,6 +92,7 @@ class OracleComparator : public gz::Comparator {
     return true;
   }
   const std::string& error() const override { return err_; }
+  int n_compare_ = 0, n_zeroing_ = 0;
 
  private:
   int w_, h_, bw_, bh_;

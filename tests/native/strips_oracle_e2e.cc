@@ -4,7 +4,10 @@
 // all-gather; every rank must produce the single-comparator bytes.  Test
 // infrastructure only.
 //
-//   strips_oracle_e2e RGB W H QUALITY WORLD OUT.jpg
+//   strips_oracle_e2e RGB W H QUALITY WORLD OUT.jpg [FAIL_RANK compare|zeroing N]
+//
+// With a failure injected into one rank's comparator (its N-th Compare or
+// zeroing call), every rank must return an error (exit 5) -- none may block.
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -80,6 +83,9 @@ int main(int argc, char** argv) {
   gz::ProcessParams params;
   params.butteraugli_target = static_cast<float>(gz::ButteraugliScoreForQuality(q));
   const gz::StripLayout L = gz::StripLayout::Make(w, h, world);
+  const int fail_rank = argc >= 10 ? atoi(argv[7]) : -1;
+  const std::string fail_kind = argc >= 10 ? argv[8] : "";
+  const int fail_at = argc >= 10 ? atoi(argv[9]) : -1;
   Exchange x(world);
   std::vector<std::string> out(world), errs(world);
   std::vector<int> rc(world, -1), iters(world, 0);
@@ -90,10 +96,13 @@ int main(int argc, char** argv) {
       gz::JpegData jpg;
       gz::EncodeRGBToJpegData(rgb.data(), w, h, &jpg);
       std::unique_ptr<gz::Comparator> inner;
-      if (L.y1[r] > L.y0[r])
-        inner.reset(new gz_test::OracleComparator(w, L.e1[r] - L.e0[r],
-                                                  rgb.data() + static_cast<size_t>(3) * w * L.e0[r],
-                                                  params.butteraugli_target));
+      if (L.y1[r] > L.y0[r]) {
+        auto* oc = new gz_test::OracleComparator(w, L.e1[r] - L.e0[r],
+                                                 rgb.data() + static_cast<size_t>(3) * w * L.e0[r],
+                                                 params.butteraugli_target);
+        if (r == fail_rank) (fail_kind == "compare" ? oc->fail_compare_at : oc->fail_zeroing_at) = fail_at;
+        inner.reset(oc);
+      }
       gz::StripComparator cmp(L, std::move(inner), &coll, params.butteraugli_target);
       gz::ProcessResult res;
       rc[r] = gz::ProcessJpegData(params, jpg, &cmp, &res, &errs[r]);
@@ -102,6 +111,13 @@ int main(int argc, char** argv) {
     });
   }
   for (auto& t : ranks) t.join();
+  if (fail_rank >= 0) {
+    for (int r = 0; r < world; ++r) {
+      printf("rank %d rc %d: %s\n", r, rc[r], errs[r].c_str());
+      if (rc[r] == 0) return 6;  // a rank missed the injected failure
+    }
+    return 5;
+  }
   for (int r = 0; r < world; ++r) {
     if (rc[r] != 0) {
       fprintf(stderr, "rank %d failed: %d %s\n", r, rc[r], errs[r].c_str());

@@ -57,7 +57,8 @@ def lib():
         L.gzo_block_diff_double.argtypes = [f64, f64, f64, f64, f64]
         L.gzo_sort_pairs.argtypes = [i32, f32, ctypes.c_int]
         L.gzo_block_zeroing_orders.argtypes = [ctypes.c_int, ctypes.c_int, u8, f32, i16, i16,
-                                               ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+                                               ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_void_p]
         L.gzo_srgb8_to_linear.argtypes = [ctypes.c_int]
         L.gzo_srgb8_to_linear.restype = ctypes.c_double
         L.gzo_init()
@@ -106,5 +107,12 @@ class Fixture:
     def rgb(self):
         return np.fromfile(self.path("input.rgb"), dtype=np.uint8)
 
-    def zero_order(self):
-        return np.fromfile(self.path("zero_order.bin"), dtype=COEFF_DTYPE).reshape(self.nb, 192)
+    def zero_order(self, variant=None):
+        """zero_order.bin, or the (lookahead, comp_mask, new_model) variant
+        zero_order_la<L>_m<M>_nm<N>.bin (make_fixtures.py zero-variants)."""
+        name = "zero_order.bin" if variant is None else "zero_order_la%d_m%d_nm%d.bin" % variant
+        return np.fromfile(self.path(name), dtype=COEFF_DTYPE).reshape(self.nb, 192)
+
+
+# (lookahead, comp_mask, new_zeroing_model) of the committed zeroing variants
+ZERO_VARIANTS = [(3, 7, 1), (1, 7, 1), (2, 7, 1), (3, 1, 1), (3, 6, 1), (3, 7, 0), (2, 6, 0)]

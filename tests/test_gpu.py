@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle_lib import COEFF_DTYPE, GOLDEN, Fixture, fixture_cases, lib as oracle
+from oracle_lib import COEFF_DTYPE, GOLDEN, ZERO_VARIANTS, Fixture, fixture_cases, lib as oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -75,12 +75,18 @@ def test_block_mask_scale_bit_exact(gz, case):
     assert bits_equal(scale, exp)
 
 
+@pytest.mark.parametrize("variant", ZERO_VARIANTS)
 @pytest.mark.parametrize("case", fixture_cases())
-def test_block_zeroing_orders_bit_exact(gz, case):
+def test_block_zeroing_orders_bit_exact(gz, case, variant):
+    """Device zeroing orders == the reference's for every committed
+    (lookahead, comp_mask, new_zeroing_model) variant; the candidate passes
+    all components (the unsearched ones keep their values in the pixels)."""
     F = Fixture(case)
+    la, mask, new_model = variant
     cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
-    out = cmp.block_zeroing_orders(F.i16("cand_coeffs.i16"), F.i16("orig_coeffs.i16"), F.target)
-    z = F.zero_order()
+    out = cmp.block_zeroing_orders(F.i16("cand_coeffs.i16"), F.i16("orig_coeffs.i16"), F.target,
+                                   comp_mask=mask, lookahead=la, new_zeroing_model=bool(new_model))
+    z = F.zero_order(None if variant == (3, 7, 1) else variant)
     assert np.array_equal(out["idx"], z["idx"]), "idx differ in %d blocks" % (
         (out["idx"] != z["idx"]).any(axis=1).sum())
     assert bits_equal(out["block_err"], z["block_err"]), mismatch(out["block_err"], z["block_err"])

@@ -60,6 +60,20 @@ def test_rgb_to_coeffs_matches_reference(gz, case):
     assert np.array_equal(c, F.i16("orig_coeffs.i16"))
 
 
+@pytest.mark.parametrize("case", fixture_cases())
+def test_block_error_adjustment_weights_match_reference(gz, case):
+    """ComputeBlockErrorAdjustmentWeights (butteraugli_comparator.cc:169-233)
+    of the reference's own distance map, both directions, radius 1..4: the
+    committed weights_d<dir>_r<r>.f32 dumps, bit for bit."""
+    F = Fixture(case)
+    dm = F.f32("distmap.f32")
+    for direction in (-1, 1):
+        for rb in range(1, 5):
+            exp = F.f32("weights_d%+d_r%d.f32" % (direction, rb))
+            got = gz.block_error_adjustment_weights(F.w, F.h, F.target, direction, rb, dm)
+            assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), (direction, rb)
+
+
 def _e2e_cases():
     cases = []
     for name, e in sorted(MANIFEST["e2e"].items()):

@@ -82,3 +82,21 @@ def test_process_jpeg_rejects_garbage():
     with pytest.raises(gz.GuetzliError) as ei:
         gz.process_jpeg(b"\xff\xd8\xff\xe0garbage", gz.Params.for_quality(95))
     assert ei.value.status == 1
+
+
+def test_oversized_sof_rejected_before_allocation():
+    """A ~20-byte file whose SOF declares 65535 x 65535 (67 M blocks per
+    component) is JPEG_IMAGE_TOO_LARGE in the reference (more than 2^21
+    blocks, jpeg_data_reader.cc:151-158): refused with INVALID_ARG before
+    any coefficient memory is allocated."""
+    import resource
+    sof = bytes([0xFF, 0xC0, 0x00, 0x11, 0x08, 0xFF, 0xFF, 0xFF, 0xFF, 0x03,
+                 0x01, 0x11, 0x00, 0x02, 0x11, 0x00, 0x03, 0x11, 0x00])
+    data = b"\xff\xd8" + sof + b"\xff\xd9"
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    with pytest.raises(gz.GuetzliError) as e:
+        gz.jpeg_decode(data)
+    assert e.value.status == gz.GZ_ERR_INVALID_ARG
+    assert "too large" in str(e.value)
+    # no multi-GB allocation happened on the way (max RSS grew < 64 MB)
+    assert resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - rss0 < 64 * 1024

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from oracle_lib import COEFF_DTYPE, Fixture, Stages, fixture_cases, lib, ROOT
+from oracle_lib import COEFF_DTYPE, ZERO_VARIANTS, Fixture, Stages, fixture_cases, lib, ROOT
 
 CASES = fixture_cases()
 
@@ -60,8 +60,11 @@ def test_oracle_compare_stages_bit_exact(case):
     assert np.float32(d) == np.float32(F.meta["distance"])
 
 
+@pytest.mark.parametrize("variant", ZERO_VARIANTS)
 @pytest.mark.parametrize("case", CASES)
-def test_oracle_block_zeroing_bit_exact(case):
+def test_oracle_block_zeroing_bit_exact(case, variant):
+    """Zeroing orders for every (lookahead, comp_mask, new_zeroing_model)
+    variant the reference was run with (processor.cc:376-487)."""
     L = lib()
     F = Fixture(case)
     w, h, n = F.w, F.h, F.w * F.h
@@ -74,9 +77,10 @@ def test_oracle_block_zeroing_bit_exact(case):
     L.gzo_mask(w, h, ref, ref, m, mdc)
     assert bits_equal(m, F.f32("ref_mask.f32"))
     out = np.zeros(F.nb * 192, COEFF_DTYPE)
+    la, mask, new_model = variant
     L.gzo_block_zeroing_orders(w, h, rgb, m, F.i16("cand_coeffs.i16"), F.i16("orig_coeffs.i16"),
-                               ctypes.c_float(F.target), 3, out.ctypes.data)
-    z = F.zero_order().ravel()
+                               ctypes.c_float(F.target), la, mask, new_model, out.ctypes.data)
+    z = F.zero_order(None if variant == (3, 7, 1) else variant).ravel()
     assert np.array_equal(out["idx"], z["idx"])
     assert bits_equal(out["block_err"], z["block_err"])
 

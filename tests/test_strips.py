@@ -108,6 +108,23 @@ def test_strip_comparator_threads_reproduce_reference(strips_e2e_bin, name, worl
     assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
 
 
+@pytest.mark.parametrize("kind,at", [("compare", 1), ("compare", 5), ("zeroing", 1)])
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_strip_rank_failure_fails_every_rank(strips_e2e_bin, kind, at, fail_rank, tmp_path):
+    """One rank's comparator fails (its at-th Compare / zeroing call): the
+    status word in every exchange makes all ranks return the error in that
+    same exchange -- none is left blocked in the next all-gather."""
+    e = MANIFEST["e2e"]["tex_64x48_q95"]
+    res = subprocess.run([strips_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]),
+                          str(e["h"]), str(e["quality"]), "2", str(tmp_path / "o.jpg"),
+                          str(fail_rank), kind, str(at)],
+                         capture_output=True, text=True, timeout=120)
+    assert res.returncode == 5, res.stdout + res.stderr
+    lines = res.stdout.strip().splitlines()
+    assert "injected" in lines[fail_rank]
+    assert "rank %d failed" % fail_rank in lines[1 - fail_rank]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
