@@ -13,16 +13,30 @@ starts.  For N > 1 (launched by torch.distributed.run, one rank per GPU)
 every rank encodes its own frames (image-level sharding, no data-path
 collective) and the JPEG byte strings are gathered to rank 0 over RCCL at
 the end of each step.  value = total pixels of all ranks / max-over-ranks
-wall time.
+wall time.  `--gpus N` without a torch.distributed.run environment starts
+the N ranks itself (one process per GPU, before any HIP call).
+
+The first timed step of every rank encodes the synthetic frames whose
+reference (`guetzli --c`) bytes are committed (tests/golden/manifest.json,
+1080p q95 seeds 0..7); they are checked after the timed region ("verified"),
+and a mismatch fails the run.
 
 Also reported (one JSON line on rank 0):
   single_frame  one frame encoded alone after the timed region (latency).
-  roofline      dominant HBM-bound kernel of the Butteraugli pass, timed with
-                HIP events on the engine's own stream inside the library
-                (gz_profile_*) during that isolated frame, against
-                algorithmic bytes per launch.
+  roofline      the kernel with the most GPU time per frame (today the
+                per-block zeroing search), timed with HIP events on the
+                engine's own stream inside the library (gz_profile_*) during
+                that isolated frame, against its algorithmic bytes per
+                launch; with its VALU issue utilisation from the committed
+                SQ counters (it is latency/VALU-bound, not HBM-bound).
+  compare_roofline  the same for the dominant kernel of the Butteraugli
+                Compare pass (block_diff), and blur_mask_pass for the
+                BASELINE blur+mask pass.
   cpu_baseline  the reference `guetzli --c` (oracle/_ref, built from the
-                reference sources) on the host cores, on a bounded sample.
+                reference sources) on the host cores: one 1080p q95 frame per
+                process, 8 concurrent processes (the bench workload's frames,
+                bytes checked against the manifest), with the host's CPU
+                model, nproc and the cores the GPU path itself consumes.
 """
 import argparse
 import concurrent.futures
@@ -65,6 +79,21 @@ def stage_bytes_per_px():
     return s
 
 
+# Per-block greedy zeroing search (k_block_zeroing), per 8x8 block: reads the
+# candidate and q=1 coefficients (2 x 3 x 64 int16), the block's RGB8 pixels
+# (192 B) and its 3 mask scales; writes its 192-entry CoeffData order (8 B
+# each) and its kept-entry count.
+ZEROING_BYTES_PER_BLOCK = 384 + 384 + 192 + 12 + 192 * 8 + 4
+
+
+def region_bytes(name, w, h):
+    """Algorithmic HBM bytes per launch of a profiled region, or None."""
+    if name == "block_zeroing":
+        return ZEROING_BYTES_PER_BLOCK * ((w + 7) // 8) * ((h + 7) // 8)
+    bpp = stage_bytes_per_px()
+    return bpp[name] * w * h if name in bpp else None
+
+
 # The "blur+mask pass" of BASELINE.json / SURVEY.md 8(d): blurs S1, S4, S7,
 # S16 and the mask chain S9-S13, 272 algorithmic B/px.  Kernels that carry
 # those stages (the opsin kernel also does the S2 transform and S3, combine the S13 LUTs with
@@ -83,6 +112,7 @@ STAGE_SYMBOL = {
     "mask_front": "gz::k_mask_stream(",
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
+    "block_zeroing": "gz::k_block_zeroing(",
     "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
 }
 
@@ -151,7 +181,24 @@ def _thread_cpu():
     return out
 
 
-def dist_setup(n_gpus):
+def launch_ranks(n_gpus):
+    """`--gpus N` outside torch.distributed.run: run this script as N ranks
+    (one process per GPU) under torch.distributed.run on 127.0.0.1 and exit
+    with its status.  Called before anything touches the GPU."""
+    import socket
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n_gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_setup(n_gpus, backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -159,43 +206,110 @@ def dist_setup(n_gpus):
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local, dist
 
 
-def cpu_baseline(width, height, quality, seconds_budget=25.0):
-    """Reference `guetzli --c` (oracle/_ref) on host cores: concurrent single-
-    threaded processes on distinct synthetic frames of the workload's kind,
-    scaled down so the sample is ~10-30 s of CPU work."""
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity_cores": len(os.sched_getaffinity(0))}
+
+
+def known_answers(w, h, q):
+    """{seed: (sha256, iterations)} of the reference's bytes for synthetic
+    frames of this size / quality (tests/golden/manifest.json)."""
+    path = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    try:
+        m = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for e in m.get("synthetic", {}).values():
+        if (e["w"], e["h"], e["quality"]) == (w, h, q):
+            out[e["seed"]] = (e["sha256"], e["iters"])
+    return out
+
+
+def cpu_baseline(width, height, quality, processes=8):
+    """Reference `guetzli --c` (oracle/_ref) on the host cores: `processes`
+    concurrent single-threaded processes (the reference has no threads), one
+    frame of the bench workload each (synthetic seeds 0.., whose reference
+    bytes are committed: checked here too), MP/s = pixels / wall."""
+    import hashlib
     ref = os.path.join(ROOT, "oracle", "_ref", "guetzli_ref")
+    info = host_info()
     if not os.path.exists(ref):
-        return {"value": None, "unit": "Mpixels/s", "cores": 0, "kind": "reference",
-                "sample": "oracle/_ref/guetzli_ref not built"}
+        return dict(info, value=None, unit="Mpixels/s", cores=0, kind="reference",
+                    sample="oracle/_ref/guetzli_ref not built")
     import guetzli_amd as gz
-    cores = max(1, min(8, len(os.sched_getaffinity(0))))
-    # ~24.5 us/px single-threaded (survey: 1080p in 47-51 s); size the frame so
-    # each process runs ~seconds_budget / cores ... capped to a quarter frame.
-    sw, sh = width // 2, height // 2
+    cores = max(1, min(processes, info["affinity_cores"]))
+    kn = known_answers(width, height, quality)
     tmp = tempfile.mkdtemp(prefix="gz_cpu_")
     procs = []
     t0 = time.time()
     for i in range(cores):
-        rgb = gz.synthetic_frame(1000 + i, sw, sh)
+        rgb = gz.synthetic_frame(i, width, height)
         path = os.path.join(tmp, "f%d.rgb" % i)
         rgb.tofile(path)
-        procs.append(subprocess.Popen([ref, "encode", path, str(sw), str(sh), str(quality),
+        procs.append(subprocess.Popen([ref, "encode", path, str(width), str(height), str(quality),
                                        os.path.join(tmp, "f%d.jpg" % i), "c"],
                                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL))
     outs = [json.loads(p.communicate()[0]) for p in procs]
     wall = time.time() - t0
-    px = cores * sw * sh
-    return {"value": px / wall / 1e6, "unit": "Mpixels/s", "cores": cores, "kind": "reference",
-            "sample": "%d concurrent single-threaded `guetzli --c` processes, one synthetic "
-                      "%dx%d q%d frame each (seeds 1000..%d), %.1f s wall, %.1f s CPU" % (
-                          cores, sw, sh, quality, 999 + cores, wall,
-                          sum(o["seconds"] for o in outs)),
-            "per_process_seconds": [round(o["seconds"], 2) for o in outs]}
+    matched = 0
+    for i in range(cores):
+        sha = hashlib.sha256(open(os.path.join(tmp, "f%d.jpg" % i), "rb").read()).hexdigest()
+        if i in kn and kn[i][0] == sha:
+            matched += 1
+    px = cores * width * height
+    return dict(info, value=px / wall / 1e6, unit="Mpixels/s", cores=cores, kind="reference",
+                sample="%d concurrent single-threaded `guetzli --c` processes, one synthetic "
+                       "%dx%d q%d frame each (seeds 0..%d: the bench workload), %.1f s wall, "
+                       "%.1f s CPU" % (cores, width, height, quality, cores - 1, wall,
+                                       sum(o["seconds"] for o in outs)),
+                per_process_seconds=[round(o["seconds"], 2) for o in outs],
+                reference_bytes_match_manifest="%d/%d" % (matched, cores))
+
+
+def dist_selftest(args):
+    """The multi-rank skeleton of main() on CPU: every rank (launched by
+    launch_ranks) joins a gloo group, "encodes" its frames into stand-in byte
+    strings (the synthetic frames' raw bytes, distinct lengths), gathers
+    them as the real run does and takes the max-over-ranks time; rank 0
+    prints one JSON line."""
+    import torch
+    import guetzli_amd as gz
+    from guetzli_amd import sharding
+    world, rank, _, dist = dist_setup(args.gpus, backend="gloo")
+    t0 = time.perf_counter()
+    blobs = [gz.synthetic_frame(rank * 100 + f, 16 + f, 8).tobytes()[:37 * (f + 1) + rank]
+             for f in range(args.frames_per_step)]
+    got = sharding.gather_bytes(blobs, dist, "cpu") if dist is not None else [blobs]
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    expect = [[gz.synthetic_frame(r * 100 + f, 16 + f, 8).tobytes()[:37 * (f + 1) + r]
+               for f in range(args.frames_per_step)] for r in range(world)]
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "gather_ok": got == expect,
+                          "max_seconds": float(t.item()),
+                          "frames": sum(len(r) for r in got)}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if got == expect else 1
 
 
 def main():
@@ -209,9 +323,18 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=8,
                     help="frames per GPU per step, encoded concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-processes", type=int, default=8)
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU check of the multi-rank path (launcher, gloo, byte gather, "
+                         "max-over-ranks timing) with stand-in payloads; no GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.dist_selftest:
+        return dist_selftest(args)
     world, rank, local, dist = dist_setup(args.gpus)
+    import hashlib
     import torch
     import guetzli_amd as gz
     from guetzli_amd import sharding
@@ -221,15 +344,21 @@ def main():
     w, h, q = args.width, args.height, args.quality
     params = gz.Params.for_quality(q)
     nsteps = args.warmup + args.steps
-    # distinct frames per (rank, step, slot), uploaded to HBM before timing
-    frames = []
+    # distinct frames per (rank, step, slot), uploaded to HBM before timing;
+    # the first timed step of every rank is the known-answer frames (seeds
+    # 0..) where the manifest has them
+    kn = known_answers(w, h, q)
+    seeds = []
     for s in range(nsteps):
         row = []
         for f in range(args.frames_per_step):
-            seed = rank * 100000 + s * 100 + f
-            rgb = gz.synthetic_frame(seed, w, h)
-            row.append(torch.from_numpy(rgb.reshape(-1)).to(f"cuda:{dev}"))
-        frames.append(row)
+            if s == args.warmup and f in kn:
+                row.append(f)
+            else:
+                row.append(1000 + rank * 100000 + s * 100 + f)
+        seeds.append(row)
+    frames = [[torch.from_numpy(gz.synthetic_frame(sd, w, h).reshape(-1)).to(f"cuda:{dev}")
+               for sd in row] for row in seeds]
     torch.cuda.synchronize()
 
     pool = concurrent.futures.ThreadPoolExecutor(max_workers=args.frames_per_step)
@@ -244,7 +373,7 @@ def main():
             # the final gather of the JPEG byte strings over RCCL/xGMI
             gathered = sharding.gather_bytes(out, dist, "cuda:%d" % dev)
             assert gathered[rank] == out
-        return [len(o) for o in out], [r[1] for r in res]
+        return out, [r[1] for r in res]
 
     for s in range(args.warmup):
         step(s)
@@ -257,10 +386,14 @@ def main():
     t0 = time.perf_counter()
     iters = []
     conc = {}
+    checked = []
     keys = ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
             "seconds_backend", "seconds_compare", "seconds_zeroing")
     for s in range(args.warmup, nsteps):
-        sizes, stats = step(s)
+        out, stats = step(s)
+        if s == args.warmup:
+            checked = [(seeds[s][f], out[f], stats[f].iterations)
+                       for f in range(len(out)) if seeds[s][f] in kn]
         iters.extend(st.iterations for st in stats)
         for st in stats:
             for k in keys:
@@ -276,12 +409,19 @@ def main():
         rows = sorted(((c - t_before.get(k, (0.0, ""))[0], n) for k, (c, n) in t_after.items()),
                       reverse=True)
         print("thread cpu:", [(round(c, 3), n) for c, n in rows[:24] if c > 0.001], file=sys.stderr)
-    cpu_per_frame = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / (
-        args.steps * args.frames_per_step)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    cpu_per_frame = cpu_s / (args.steps * args.frames_per_step)
+    # verification of the known-answer frames (after the timed region)
+    ok = sum(1 for sd, data, it in checked
+             if (hashlib.sha256(data).hexdigest(), it) == kn[sd])
+    counts = [len(checked), ok]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        c = torch.tensor(counts, dtype=torch.int64, device=f"cuda:{dev}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        counts = [int(v) for v in c.tolist()]
 
     # isolated frame: latency, host breakdown and per-kernel HIP-event timing
     gz.profile_reset()
@@ -292,8 +432,7 @@ def main():
     gz.profile_enable(False)
     prof = gz.profile_read()
     host = {}
-    for k in ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
-              "seconds_backend", "seconds_compare", "seconds_zeroing"):
+    for k in keys:
         host[k] = getattr(st1, k)
     host.update(gz.last_process_detail())
 
@@ -305,33 +444,48 @@ def main():
     total_px = world * args.steps * args.frames_per_step * w * h
     value = total_px / elapsed / 1e6
 
-    # roofline of the dominant kernel of the Butteraugli pass (by total time
-    # in the isolated, HIP-event-timed frame)
     bpp = stage_bytes_per_px()
-    rows = []
-    for name, (cnt, ms) in prof.items():
-        if name in bpp and cnt:
-            rows.append((ms, name, cnt))
-    rows.sort(reverse=True)
-    roof = None
     stages = {}
-    for ms, name, cnt in rows:
+    regions = []
+    for name, (cnt, ms) in prof.items():
+        if not cnt:
+            continue
         avg = ms / cnt
-        gbs = bpp[name] * w * h / (avg * 1e-3) / 1e9
-        stages[name] = {"launches": cnt, "avg_ms": round(avg, 4), "algo_GBps": round(gbs, 1)}
-    if rows:
-        ms, name, cnt = rows[0]
+        b = region_bytes(name, w, h)
+        row = {"launches": cnt, "avg_ms": round(avg, 4), "frame_ms": round(ms, 4)}
+        if b is not None:
+            row["algo_GBps"] = round(b / (avg * 1e-3) / 1e9, 1)
+        if name in bpp or name == "block_zeroing":
+            stages[name] = row
+        if name != "compare_pass":
+            regions.append((ms, name, cnt))
+    regions.sort(reverse=True)
+
+    def roof_of(name):
+        cnt, ms = prof[name]
         avg = ms / cnt
-        achieved = bpp[name] * w * h / (avg * 1e-3) / 1e9
+        b = region_bytes(name, w, h)
+        achieved = b / (avg * 1e-3) / 1e9
         traffic, tsrc = measured_traffic(name, w, h)
-        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "traffic_source": tsrc,
-                "algo_bytes_per_launch": int(bpp[name] * w * h),
-                "avg_launch_ms": round(avg, 4)}
+        r = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+             "traffic": traffic, "traffic_source": tsrc, "algo_bytes_per_launch": int(b),
+             "avg_launch_ms": round(avg, 4), "launches_per_frame": cnt,
+             "frame_gpu_ms": round(ms, 4)}
         vi = valu_issue(name, w, h, avg)
         if vi:
-            roof["valu_issue"] = vi
+            r["valu_issue"] = vi
+        return r
+
+    # the roofline line: the kernel with the most GPU time in the frame
+    dominant = next((n for _, n, _ in regions if region_bytes(n, w, h) is not None), None)
+    roof = roof_of(dominant) if dominant else None
+    if roof is not None:
+        roof["gpu_time_share_of_frame"] = round(
+            prof[dominant][1] / sum(ms for ms, _, _ in regions), 4)
+    # the dominant kernel of the Butteraugli Compare pass
+    cmp_rows = sorted(((prof[n][1], n) for n in bpp if n in prof and prof[n][0]), reverse=True)
+    compare_roof = roof_of(cmp_rows[0][1]) if cmp_rows else None
     bm_ms = sum(stages[k]["avg_ms"] for k in BLUR_MASK_STAGES if k in stages)
     blur_mask = None
     if bm_ms > 0:
@@ -354,7 +508,7 @@ def main():
         compare_pass = {"launches": cp[0], "avg_ms": round(avg, 4),
                         "algo_bytes": int(pass_bytes),
                         "algo_GBps": round(pass_bytes / (avg * 1e-3) / 1e9, 1)}
-    bz = prof.get("block_zeroing")
+    gpu_frame_ms = sum(ms for ms, _, _ in regions)
 
     out = {
         "metric": METRIC,
@@ -378,24 +532,33 @@ def main():
                    "parallelism": "image-sharded over %d GPU(s)%s" % (
                        world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
                    "search_iterations": iters},
+        "verified": {"frames": counts[0], "bit_exact": counts[1],
+                     "against": "reference guetzli --c sha256 + iterations "
+                                "(tests/golden/manifest.json)"},
         "roofline": roof,
+        "compare_roofline": compare_roof,
         "compare_pass": compare_pass,
         "blur_mask_pass": blur_mask,
-        "block_zeroing": {"launches": bz[0], "avg_ms": round(bz[1] / bz[0], 3)} if bz else None,
         "stages": stages,
+        "gpu_ms_per_frame_isolated": round(gpu_frame_ms, 3),
         "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
         "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
+        "host_cores_busy_per_gpu": round(cpu_s / elapsed, 2),
         "single_frame": {"seconds": round(single_s, 4),
                          "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
                          "iterations": st1.iterations,
                          "host_breakdown_seconds": {k: round(v, 4) for k, v in host.items()}},
     }
     if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(w, h, q)
-    print(json.dumps(out))
+        out["cpu_baseline"] = cpu_baseline(w, h, q, args.cpu_baseline_processes)
+    print(json.dumps(out), flush=True)
     pool.shutdown()
     if dist is not None:
         dist.destroy_process_group()
+    if counts[1] != counts[0]:
+        print("bench: %d of %d known-answer frames differ from the reference" % (
+            counts[0] - counts[1], counts[0]), file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

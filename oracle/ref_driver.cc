@@ -6,7 +6,8 @@
 // dumps end-to-end JPEG bytes and stage-level intermediates that the clean-room
 // restatement (oracle/gz_oracle.c) and the HIP product are pinned against.
 //
-//   guetzli_ref encode  RGB W H QUALITY OUT.jpg [c|cpu]     guetzli.cc:247-368
+//   guetzli_ref encode  RGB W H QUALITY OUT.jpg [c|cpu] [lookahead=N new_model=0|1
+//                       try_420=0|1 force_420=0|1]       guetzli.cc:247-368
 //   guetzli_ref stages  RGB W H QSEED OUTDIR                 see Stages()
 //   guetzli_ref zero_variants RGB W H QSEED OUTDIR           see ZeroVariants()
 //   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg            processor.cc:1029-1066
@@ -91,6 +92,19 @@ int Encode(int argc, char** argv) {
   guetzli::Params params;
   params.butteraugli_target =
       static_cast<float>(guetzli::ButteraugliScoreForQuality(quality));
+  // optional Params overrides: lookahead=N new_model=0|1 try_420=0|1 force_420=0|1
+  for (int i = 8; i < argc; ++i) {
+    const std::string kv = argv[i];
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) return 1;
+    const std::string k = kv.substr(0, eq);
+    const int v = atoi(kv.c_str() + eq + 1);
+    if (k == "lookahead") params.zeroing_greedy_lookahead = v;
+    else if (k == "new_model") params.new_zeroing_model = v != 0;
+    else if (k == "try_420") params.try_420 = v != 0;
+    else if (k == "force_420") params.force_420 = v != 0;
+    else return 1;
+  }
   guetzli::ProcessStats stats;
   std::string out;
   auto t0 = std::chrono::steady_clock::now();

@@ -101,17 +101,23 @@ def run_zero_variants():
         print("zero variants", name)
 
 
-def run_e2e(manifest, cases):
-    out = manifest.setdefault("e2e", {})
-    for name, rgb, w, h, q in cases:
+def run_e2e(manifest, cases, section="e2e"):
+    """cases: (name, rgb path, w, h, quality[, {Params overrides}])."""
+    out = manifest.setdefault(section, {})
+    for case in cases:
+        name, rgb, w, h, q = case[:5]
+        params = case[5] if len(case) > 5 else {}
         jpg = "/tmp/gz_fixture_%s.jpg" % name
-        res = subprocess.run([REF, "encode", rgb, str(w), str(h), str(q), jpg, "c"], check=True,
+        res = subprocess.run([REF, "encode", rgb, str(w), str(h), str(q), jpg, "c"] +
+                             ["%s=%d" % kv for kv in sorted(params.items())], check=True,
                              capture_output=True, text=True)
         info = json.loads(res.stdout)
         out[name] = {"w": w, "h": h, "quality": q, "sha256": sha256(jpg), "bytes": info["bytes"],
                      "iters": info["iters"], "ref_seconds": info["seconds"],
                      "input": os.path.relpath(rgb, HERE) if rgb.startswith(HERE) else rgb}
-        print("e2e", name, out[name])
+        if params:
+            out[name]["params"] = params
+        print(section, name, out[name])
 
 
 def main():
@@ -132,6 +138,16 @@ def main():
         cases.append(("bees_q90", os.path.join(HERE, "bees.rgb"), 444, 258, 90))
         cases.append(("bees_q84", os.path.join(HERE, "bees.rgb"), 444, 258, 84))
         run_e2e(manifest, cases)
+    if "e2e-params" in what:
+        # Params variants: old zeroing model, lookahead 1 / 2 (processor.cc:400-405, :416)
+        bees = os.path.join(HERE, "bees.rgb")
+        tex = os.path.join(HERE, "stages_tex_100x77", "input.rgb")
+        run_e2e(manifest, [
+            ("bees_q95_oldmodel", bees, 444, 258, 95, {"new_model": 0}),
+            ("bees_q90_lookahead1", bees, 444, 258, 90, {"lookahead": 1}),
+            ("tex_100x77_q95_oldmodel", tex, 100, 77, 95, {"new_model": 0}),
+            ("tex_100x77_q95_lookahead2", tex, 100, 77, 95, {"lookahead": 2}),
+        ], section="e2e_params")
     json.dump(manifest, open(manifest_path, "w"), indent=1, sort_keys=True)
 
 

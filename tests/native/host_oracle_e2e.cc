@@ -19,7 +19,7 @@ using gz_test::OracleComparator;
 
 int main(int argc, char** argv) {
   if (argc < 6) {
-    fprintf(stderr, "usage: host_oracle_e2e RGB W H QUALITY OUT.jpg\n");
+    fprintf(stderr, "usage: host_oracle_e2e RGB W H QUALITY OUT.jpg [lookahead=N] [new_model=0|1]\n");
     return 1;
   }
   FILE* f = fopen(argv[1], "rb");
@@ -30,6 +30,16 @@ int main(int argc, char** argv) {
   fclose(f);
   gz::ProcessParams params;
   params.butteraugli_target = static_cast<float>(gz::ButteraugliScoreForQuality(q));
+  // optional Params overrides (as oracle/ref_driver encode): lookahead=N new_model=0|1
+  for (int i = 6; i < argc; ++i) {
+    const std::string kv = argv[i];
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) return 1;
+    const int v = atoi(kv.c_str() + eq + 1);
+    if (kv.compare(0, eq, "lookahead") == 0) params.zeroing_greedy_lookahead = v;
+    else if (kv.compare(0, eq, "new_model") == 0) params.new_zeroing_model = v != 0;
+    else return 1;
+  }
   gz::JpegData jpg;
   gz::EncodeRGBToJpegData(rgb.data(), w, h, &jpg);
   OracleComparator cmp(w, h, rgb.data(), params.butteraugli_target);

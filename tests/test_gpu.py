@@ -207,3 +207,75 @@ def test_compare_fast_path_matches_oracle(gz, w, h, seed):
     bm = np.array([max(0.0, dm[8 * by:8 * by + 8, 8 * bx:8 * bx + 8].max())
                    for by in range(bh) for bx in range(bw)], np.float32)
     assert bits_equal(cmp.block_max(), bm)
+
+
+def _known_answer_jobs(gz):
+    """Distinct inputs with the reference's known answers: synthetic 1080p
+    q95 seeds 0..7 (BASELINE configs[1]/[3] frames) and bees at q95/q90/q84."""
+    jobs = []
+    for s in range(8):
+        e = MANIFEST["synthetic"]["synth_1920x1080_s%d_q95" % s]
+        jobs.append(("synth_s%d" % s, gz.synthetic_frame(s, 1920, 1080), 1920, 1080, 95, e))
+    for name in ("bees_q95", "bees_q90", "bees_q84"):
+        e = MANIFEST["e2e"][name]
+        rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+        jobs.append((name, rgb, e["w"], e["h"], e["quality"], e))
+    return jobs
+
+
+@pytest.mark.parametrize("threads", [8, 11])
+def test_concurrent_encodes_known_answers(gz, threads):
+    """configs[3]'s per-GPU shape: several encodes in flight on one GPU at
+    once (one host thread + engine + stream each, sharing the engine pool,
+    the host worker pool and the device entropy coder), inputs in HBM
+    (gz_process_rgb_device, as bench.py) and in host memory: every output is
+    byte-identical to the reference's, twice over (the second round reuses
+    pooled engines)."""
+    import concurrent.futures
+    import torch
+    jobs = _known_answer_jobs(gz)[:threads]
+    dev = [torch.from_numpy(np.ascontiguousarray(j[1]).reshape(-1)).to("cuda:0") for j in jobs]
+    torch.cuda.synchronize()
+
+    def run(i):
+        name, rgb, w, h, q, e = jobs[i]
+        p = gz.Params.for_quality(q)
+        if i % 2 == 0:
+            data, st = gz.process_device(dev[i].data_ptr(), w, h, p, return_stats=True)
+        else:
+            data, st = gz.process(rgb, w, h, p, return_stats=True)
+        return name, hashlib.sha256(data).hexdigest(), st.iterations
+
+    with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as ex:
+        for _ in range(2):
+            for name, sha, iters in ex.map(run, range(len(jobs))):
+                e = jobs[[j[0] for j in jobs].index(name)][5]
+                assert (sha, iters) == (e["sha256"], e["iters"]), name
+
+
+def test_engine_pool_trim(gz):
+    """Encodes leave their engines pooled; trim releases them (LRU, byte
+    accounting) and the next encode re-creates one with the same bytes."""
+    e = MANIFEST["e2e"]["bees_q95"]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    gz.process(rgb, e["w"], e["h"], gz.Params.for_quality(95))
+    assert gz.engine_pool_idle_bytes() > 0
+    freed = gz.engine_pool_trim(0)
+    assert freed > 0 and gz.engine_pool_idle_bytes() == 0
+    data = gz.process(rgb, e["w"], e["h"], gz.Params.for_quality(95))
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]
+    assert gz.engine_pool_idle_bytes() > 0
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST.get("e2e_params", {})))
+def test_process_params_variants_known_answers(gz, name):
+    """Params::new_zeroing_model = false and zeroing_greedy_lookahead 1 / 2
+    (processor.cc:400-405, :416) end to end: the reference's bytes."""
+    e = MANIFEST["e2e_params"][name]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    p = gz.Params.for_quality(e["quality"])
+    p.zeroing_greedy_lookahead = e["params"].get("lookahead", 3)
+    p.new_zeroing_model = bool(e["params"].get("new_model", 1))
+    data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
+    assert st.iterations == e["iters"]
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]

@@ -82,12 +82,21 @@ def _e2e_cases():
     return cases
 
 
-@pytest.mark.parametrize("name", _e2e_cases())
-def test_host_loop_with_oracle_comparator_bit_exact(host_e2e_bin, name, tmp_path):
-    e = MANIFEST["e2e"][name]
+def _e2e_params_cases():
+    return [("e2e_params", n) for n, e in sorted(MANIFEST.get("e2e_params", {}).items())
+            if e["w"] * e["h"] <= 100 * 100]
+
+
+@pytest.mark.parametrize("section,name", [("e2e", n) for n in _e2e_cases()] + _e2e_params_cases())
+def test_host_loop_with_oracle_comparator_bit_exact(host_e2e_bin, section, name, tmp_path):
+    """Product host loop + CPU-oracle comparator == the reference's bytes,
+    including the Params variants (old zeroing model, lookahead 1 / 2)."""
+    e = MANIFEST[section][name]
     out = tmp_path / "out.jpg"
     res = subprocess.run([host_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]), str(e["h"]),
-                          str(e["quality"]), str(out)], capture_output=True, text=True, timeout=600)
+                          str(e["quality"]), str(out)] +
+                         ["%s=%d" % kv for kv in sorted(e.get("params", {}).items())],
+                         capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr
     info = json.loads(res.stdout)
     assert info["iters"] == e["iters"]

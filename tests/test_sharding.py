@@ -61,3 +61,25 @@ def test_gather_bytes_world2():
         assert lens == expect
         assert own_ok
     assert res[0][3] == res[1][3]
+
+
+def test_bench_launches_ranks_itself_world2():
+    """`bench.py --gpus 2` outside torch.distributed.run starts the two ranks
+    itself (torch.distributed.run on 127.0.0.1, one process per GPU); the CPU
+    self-test mode runs the same launcher, process group, byte gather and
+    max-over-ranks timing over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--frames-per-step", "3", "--dist-selftest"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-2000:]
+    line = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, res.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and out["gather_ok"] and out["frames"] == 6
