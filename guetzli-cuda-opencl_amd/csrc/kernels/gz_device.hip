@@ -89,14 +89,20 @@ void BuildBlur(float sigma, float border_ratio, BlurSpec* b) {
   b->weight_no_border = wnb;
 }
 
+static_assert(kFixCrR == 91881 && kFixCbB == 116130 && kFixCrG == 46802 && kFixCbG == 22554,
+              "libjpeg YCbCr->RGB fixed-point constants");
+
 void BuildTables(GzTables* t) {
+  if (Fix16(1.40200) != kFixCrR || Fix16(1.77200) != kFixCbB || Fix16(0.71414) != kFixCrG ||
+      Fix16(0.34414) != kFixCbG)
+    abort();  // the device forms the YCbCr tables from these constants
   memset(t, 0, sizeof(*t));
   for (int i = 0; i < 256; ++i) {
     const double lin =
         i < 11 ? i / 12.92 : 255.0 * pow(((i / 255.0) + 0.055) / 1.055, 2.4);  // gamma_correct.cc:27-33
     t->srgb[i] = static_cast<float>(lin);
     const int x = i - 128;  // libjpeg build_ycc_rgb_table (color_transform.h tables)
-    t->cr_r[i] = (Fix16(1.40200) * x + 32768) >> 16;
+    t->cr_r[i] = (Fix16(1.40200) * x + 32768) >> 16;  // == (kFixCrR * x + 32768) >> 16 on the device
     t->cb_b[i] = (Fix16(1.77200) * x + 32768) >> 16;
     t->cr_g[i] = -Fix16(0.71414) * x;
     t->cb_g[i] = -Fix16(0.34414) * x + 32768;
@@ -899,13 +905,6 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
                                 CoeffDataHost* out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  unsigned long long* timers = nullptr;
-  if (getenv("GZ_ZEROING_TIMERS")) {  // debug: per-phase cycle totals on stderr
-    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&timers), 16 * 8));
-    GZ_HIP(hipMemsetAsync(timers, 0, 16 * 8, s));
-    GZ_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_bz_timers), &timers, sizeof(timers), 0,
-                                  hipMemcpyHostToDevice, s));
-  }
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
@@ -915,16 +914,6 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
-  if (timers) {
-    unsigned long long t[16];
-    GZ_HIP(hipMemcpy(t, timers, sizeof(t), hipMemcpyDeviceToHost));
-    unsigned long long* null_ptr = nullptr;
-    GZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bz_timers), &null_ptr, sizeof(null_ptr)));
-    GZ_HIP(hipFree(timers));
-    fprintf(stderr, "zeroing phase cycles (lane 0, summed over blocks; [15] = evaluations):");
-    for (int i = 0; i < 16; ++i) fprintf(stderr, " %d:%llu", i, t[i]);
-    fprintf(stderr, "\n");
-  }
   return true;
 }
 

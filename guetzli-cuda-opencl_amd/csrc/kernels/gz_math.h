@@ -246,12 +246,13 @@ __device__ __forceinline__ void lowfreq_sq_f(const float a[3], const float b[3],
 }
 
 __device__ __forceinline__ void lowfreq_sq_zero_d(double x, double y, double z, double factor,
-                                                  double res[3]) {
+                                                  double res[3],
+                                                  const double* lf_dy = c_tab.lf_dy_d) {
   // butteraugli.cc:305-340 (double)
   z += 0.0812519812628 * y;
   const double vz = z * 7.34905756986;
   const double vx = x * 6.64482198135;
-  const double vy = interp_d(c_tab.lf_dy_d, 21, y * 0.837846224276);
+  const double vy = interp_d(lf_dy, 21, y * 0.837846224276);
   res[0] += factor * vx * vx;
   res[1] += factor * vy * vy;
   res[2] += factor * vz * vz;
@@ -393,6 +394,10 @@ __device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], c
 // ---------------------------------------------------------------------------
 
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// libjpeg build_ycc_rgb_table fixed-point factors FIX(x) = int(x * 2^16 + 0.5)
+// (color_transform.h tables): 1.40200, 1.77200, 0.71414, 0.34414.
+constexpr int kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554;
 
 __device__ __forceinline__ void ycbcr_to_linear(int y, int cb, int cr, float out[3]) {
   const int r = clamp255(y + c_tab.cr_r[cr]);

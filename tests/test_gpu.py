@@ -232,25 +232,40 @@ def test_concurrent_encodes_known_answers(gz, threads):
     byte-identical to the reference's, twice over (the second round reuses
     pooled engines)."""
     import concurrent.futures
-    import torch
+    import ctypes
     jobs = _known_answer_jobs(gz)[:threads]
-    dev = [torch.from_numpy(np.ascontiguousarray(j[1]).reshape(-1)).to("cuda:0") for j in jobs]
-    torch.cuda.synchronize()
+    # device copies of the inputs through the HIP runtime the library itself
+    # uses (already loaded with it: same soname)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    dev = []
+    for j in jobs:
+        a = np.ascontiguousarray(j[1]).reshape(-1)
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), a.nbytes) == 0
+        assert hip.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0  # hipMemcpyHostToDevice
+        dev.append(p)
 
     def run(i):
         name, rgb, w, h, q, e = jobs[i]
         p = gz.Params.for_quality(q)
         if i % 2 == 0:
-            data, st = gz.process_device(dev[i].data_ptr(), w, h, p, return_stats=True)
+            data, st = gz.process_device(dev[i].value, w, h, p, return_stats=True)
         else:
             data, st = gz.process(rgb, w, h, p, return_stats=True)
         return name, hashlib.sha256(data).hexdigest(), st.iterations
 
-    with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as ex:
-        for _ in range(2):
-            for name, sha, iters in ex.map(run, range(len(jobs))):
-                e = jobs[[j[0] for j in jobs].index(name)][5]
-                assert (sha, iters) == (e["sha256"], e["iters"]), name
+    try:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as ex:
+            for _ in range(2):
+                for name, sha, iters in ex.map(run, range(len(jobs))):
+                    e = jobs[[j[0] for j in jobs].index(name)][5]
+                    assert (sha, iters) == (e["sha256"], e["iters"]), name
+    finally:
+        for p in dev:
+            hip.hipFree(p)
 
 
 def test_engine_pool_trim(gz):
