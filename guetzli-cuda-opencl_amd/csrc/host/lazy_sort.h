@@ -36,8 +36,43 @@ class LazyStdSort {
     }
   }
 
-  // a[0..sorted()) already hold their final std::sort values.
+  // a[0..sorted()) already hold their final std::sort values (or, below a
+  // SetPrefix boundary, their final values as a set).
   size_t sorted() const { return done_; }
+
+  // After this, a[0..p) hold the first p values of std::sort's result as a
+  // set (in no particular order) and a[p..sorted()) their final values:
+  // ranges that lie wholly inside [0, p) are dropped unsorted -- they are
+  // leaves of the partition tree whose membership is already final -- and
+  // only a range straddling p is refined (partitioned, or finished as a leaf).
+  void SetPrefix(size_t p) {
+    while (!pending_.empty()) {
+      const Range r = pending_.back();
+      if (r.hi <= p) {
+        pending_.pop_back();
+        done_ = r.hi;
+        continue;
+      }
+      if (r.lo >= p) break;
+      pending_.pop_back();
+      Elem* f = a_ + r.lo;
+      Elem* l = a_ + r.hi;
+      if (r.hi - r.lo <= kThreshold) {
+        InsertionSort(f, l);
+        done_ = r.hi;
+      } else if (r.depth == 0) {
+        HeapSort(f, l);
+        done_ = r.hi;
+      } else {
+        Elem* mid = f + (l - f) / 2;
+        MoveMedianToFirst(f, f + 1, mid, l - 1);
+        const size_t cut = static_cast<size_t>(UnguardedPartition(f + 1, l, f) - a_);
+        pending_.push_back(Range{cut, r.hi, r.depth - 1});
+        pending_.push_back(Range{r.lo, cut, r.depth - 1});
+      }
+    }
+    if (done_ < p) done_ = p;
+  }
 
   // After this, a[0..i] hold their final std::sort values.
   void EnsureSorted(size_t i) {

@@ -737,6 +737,9 @@ class Processor {
   size_t best_size_ = 0;
   double encode_s_ = 0.0;
   double final_score_ = -1;
+  std::vector<int> bulk_cnt_;  // per-block change counts of a back-end bulk prefix
+  static constexpr int kOrderChunk = 1024;     // blocks per parallel back-end work item
+  static constexpr size_t kMinBulkChanges = 64;
 };
 
 bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
@@ -854,25 +857,54 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const std::vector<float>& bmax = first_up_iter ? zero_block_max : cmp_->block_max_distance();
         cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, 1, 1, bmax,
                                                  &block_weight);
-        global_order.clear();
-        blocks_to_change = 0;
-        for (int bix = 0; bix < num_blocks; ++bix) {
+        // the candidate entries of every block in block order (processor.cc:
+        // 806-829), built in parallel over chunks of blocks: entry counts,
+        // their prefix sums, then each chunk fills its own range
+        const int nchunks = (num_blocks + kOrderChunk - 1) / kOrderChunk;
+        std::vector<size_t> chunk_start(nchunks + 1, 0);
+        std::vector<int> chunk_btc(nchunks, 0);
+        auto block_entries = [&](int bix) -> int {
+          if (block_weight[bix] == 0) return 0;
           const int last_index = last_indexes[bix];
           const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
           const int num_candidates = offsets[bix + 1] - offset;
-          const float* errs = cand_err.data() + offset;
-          const float max_err = max_block_error[bix];
-          if (block_weight[bix] == 0) continue;
-          if (direction > 0) {
-            for (size_t i = last_index; i < static_cast<size_t>(num_candidates); ++i)
-              global_order.push_back(std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]));
-            blocks_to_change += last_index < num_candidates ? 1 : 0;
-          } else {
-            for (int i = last_index - 1; i >= 0; --i)
-              global_order.push_back(std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]));
-            blocks_to_change += last_index > 0 ? 1 : 0;
+          return direction > 0 ? std::max(0, num_candidates - last_index) : last_index;
+        };
+        ParallelFor(nchunks, [&](int ch) {
+          size_t n = 0;
+          int btc = 0;
+          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+            const int e = block_entries(bix);
+            n += e;
+            btc += e > 0 ? 1 : 0;
           }
+          chunk_start[ch + 1] = n;
+          chunk_btc[ch] = btc;
+        });
+        blocks_to_change = 0;
+        for (int ch = 0; ch < nchunks; ++ch) {
+          chunk_start[ch + 1] += chunk_start[ch];
+          blocks_to_change += chunk_btc[ch];
         }
+        global_order.resize(chunk_start[nchunks]);
+        ParallelFor(nchunks, [&](int ch) {
+          std::pair<int, float>* out = global_order.data() + chunk_start[ch];
+          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+            if (block_weight[bix] == 0) continue;
+            const int last_index = last_indexes[bix];
+            const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
+            const int num_candidates = offsets[bix + 1] - offset;
+            const float* errs = cand_err.data() + offset;
+            const float max_err = max_block_error[bix];
+            if (direction > 0) {
+              for (int i = last_index; i < num_candidates; ++i)
+                *out++ = std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]);
+            } else {
+              for (int i = last_index - 1; i >= 0; --i)
+                *out++ = std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]);
+            }
+          }
+        });
         if (!global_order.empty()) break;
       }
       res_->detail["backend_order_s"] += Since(tb);
@@ -901,6 +933,66 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       float val_threshold = 0.0f;
       int changed_coeffs = 0;
       int est_jpg_size = prev_size;
+      // Changes before the loop's first read of an entropy code or size
+      // estimate (first_read: the first i % 10 == 0 step whose codes are
+      // read, the first step with changed_coeffs > min_coeffs_to_change, or
+      // the last one) only accumulate; their effect -- block states, AC
+      // histograms, last_indexes -- depends on which changes they are, not
+      // on their order.  So [0, first_read) is taken as std::sort's first
+      // first_read entries as a set (LazyStdSort::SetPrefix: partitioning
+      // only, no sort of the prefix) and applied per block in parallel.
+      size_t bulk = 0;
+      {
+        const long m = std::max(0, min_coeffs_to_change);
+        const long n = static_cast<long>(global_order.size());
+        const long lo = std::max(0L, std::min(m - 9, n - 10));
+        const long first_code = (lo + 9) / 10 * 10;
+        const long first_read = std::min(std::min(first_code, m), n - 1);
+        if (first_read >= kMinBulkChanges) bulk = static_cast<size_t>(first_read);
+      }
+      if (bulk) {
+        const auto tbk = Clock::now();
+        sorter.SetPrefix(bulk);
+        bulk_cnt_.assign(num_blocks, 0);
+        for (size_t i = 0; i < bulk; ++i) ++bulk_cnt_[global_order[i].first];
+        const int nchunks = (num_blocks + kOrderChunk - 1) / kOrderChunk;
+        struct ChunkDelta {
+          JpegHistogram h[3];
+          std::vector<uint32_t> changed;
+        };
+        std::vector<ChunkDelta> deltas(nchunks);
+        ParallelFor(nchunks, [&](int ch) {
+          ChunkDelta& d = deltas[ch];
+          int64_t raw_unused = 0;
+          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+            const int cnt = bulk_cnt_[bix];
+            if (!cnt) continue;
+            const int bx = bix % block_width, by = bix / block_width;
+            const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+            for (int t = 0; t < cnt; ++t) {
+              const int idx = cand[offset + last_indexes[bix] + std::min(direction, 0)];
+              const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+              const int* quant = img->quant[c];
+              const JpegComponent& comp = jpg.components[c];
+              const int jpg_bix = by * comp.width_in_blocks + bx;
+              const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
+              acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
+                         &ac_depths[c * JpegHistogram::kSize], &d.h[c], &raw_unused);
+              d.changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * num_blocks + bix) * 64 + k));
+              last_indexes[bix] += direction;
+            }
+          }
+        });
+        for (const ChunkDelta& d : deltas) {
+          for (int c = 0; c < ncomp && c < 3; ++c)
+            for (int q = 0; q < JpegHistogram::kSize; ++q) ac_histograms[c].counts[q] += d.h[c].counts[q];
+          img->changed.insert(img->changed.end(), d.changed.begin(), d.changed.end());
+        }
+        refresh_raw();
+        changed_coeffs = static_cast<int>(bulk);
+        res_->detail["backend_bulk_s"] += Since(tbk);
+        res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+      }
       // The size estimate only matters once changed_coeffs > min_coeffs_to_change
       // and at the last step (it becomes prev_size); the entropy codes it uses
       // are those of the last i % 10 == 0 step.  Codes of decades that contain
@@ -914,7 +1006,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // then the coefficient block and its non-zero mask -- so the cache
       // misses of a chunk overlap instead of chaining.  Values are only
       // prefetched; the loop below reads them as before.
-      size_t prefetched = 0;
+      size_t prefetched = bulk;
       auto prefetch_chunk = [&](size_t lo, size_t hi) {
         for (size_t j = lo; j < hi; ++j) {
           const int b = global_order[j].first;
@@ -938,7 +1030,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
       };
       double sort_s = 0.0;
-      for (size_t i = 0; i < n_order; ++i) {
+      for (size_t i = bulk; i < n_order; ++i) {
         if (i >= sorter.sorted()) {
           const auto ts = Clock::now();
           sorter.EnsureSorted(i);

@@ -31,6 +31,29 @@ int main(int argc, char** argv) {
       s.EnsureSorted(a.size());
       if (a != ref) ++bad;
       ++cases;
+      // SetPrefix(p): a[0..p) is std::sort's first p as a multiset, the rest
+      // (materialised later) exactly std::sort's
+      {
+        std::vector<std::pair<int, float>> b(n);
+        for (int i = 0; i < n; ++i) b[i] = {i, static_cast<float>(rng() % static_cast<unsigned>(distinct)) * 0.5f};
+        auto rb = b;
+        std::sort(rb.begin(), rb.end(),
+                  [](const std::pair<int, float>& x, const std::pair<int, float>& y) { return x.second < y.second; });
+        gz::LazyStdSort t(b.data(), b.size());
+        const size_t p = n ? static_cast<size_t>(rng() % (n + 1)) : 0;
+        t.SetPrefix(p);
+        auto head = std::vector<std::pair<int, float>>(b.begin(), b.begin() + p);
+        auto rhead = std::vector<std::pair<int, float>>(rb.begin(), rb.begin() + p);
+        std::sort(head.begin(), head.end());
+        std::sort(rhead.begin(), rhead.end());
+        if (head != rhead || t.sorted() < p) ++bad;
+        for (size_t i = p; i < t.sorted() && i < b.size(); ++i)
+          if (b[i] != rb[i]) { ++bad; break; }
+        if (n) t.EnsureSorted(b.size() - 1);
+        for (size_t i = p; i < b.size(); ++i)
+          if (b[i] != rb[i]) { ++bad; break; }
+        ++cases;
+      }
     }
   }
   printf("{\"cases\": %d, \"bad\": %d}\n", cases, bad);
