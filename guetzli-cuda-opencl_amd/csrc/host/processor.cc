@@ -8,6 +8,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 #include <thread>
@@ -984,8 +986,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           }
         });
         for (const ChunkDelta& d : deltas) {
+          // (symbols only: the last slot is the histogram's fixed sentinel count)
           for (int c = 0; c < ncomp && c < 3; ++c)
-            for (int q = 0; q < JpegHistogram::kSize; ++q) ac_histograms[c].counts[q] += d.h[c].counts[q];
+            for (int q = 0; q + 1 < JpegHistogram::kSize; ++q) ac_histograms[c].counts[q] += d.h[c].counts[q];
           img->changed.insert(img->changed.end(), d.changed.begin(), d.changed.end());
         }
         refresh_raw();
@@ -1075,6 +1078,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       res_->detail["backend_sort_s"] += sort_s;
       res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += changed_coeffs;
+      if (getenv("GZ_DEBUG_BACKEND")) fprintf(stderr, "iter dir %d n %zu min %d bulk %zu changed %d thr %.9g est %d prev %d\n", direction, n_order, min_coeffs_to_change, bulk, changed_coeffs, val_threshold, est_jpg_size, prev_size);
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
