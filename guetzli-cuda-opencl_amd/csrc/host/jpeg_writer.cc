@@ -162,22 +162,37 @@ void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t
   // Huffman tree with iterative count flattening until it fits max_depth
   // (CreateHuffmanTree, entropy_encode.cc:65-145).  Leaves sorted by
   // (count asc, symbol desc): a total order, so any correct sort agrees --
-  // here a sort of packed 64-bit keys.
+  // here a sort of packed 64-bit keys.  Each retry raises every count below
+  // count_limit to it: the leaves with count <= count_limit (a prefix of the
+  // first attempt's order) become one group ordered by symbol alone, the
+  // rest keep their order, so a retry re-sorts only that prefix.  A try's
+  // tree height is tracked while it is built; depths are assigned only for
+  // the tree that fits -- the same tree, leaf order and merges as the
+  // reference's loop, so the same depths.
   TreeNode tree[2 * JpegHistogram::kSize + 2];
-  uint64_t keys[JpegHistogram::kSize];
+  uint8_t height[2 * JpegHistogram::kSize + 2];
+  uint64_t base[JpegHistogram::kSize], keys[JpegHistogram::kSize];
+  int n = 0;
+  for (int i = length - 1; i >= 0; --i)
+    if (data[i]) base[n++] = (static_cast<uint64_t>(data[i]) << 16) | (0xffff - i);
+  if (n == 0) return;
+  if (n == 1) {
+    depth[0xffff - (base[0] & 0xffff)] = 1;
+    return;
+  }
+  std::sort(base, base + n);
   for (uint32_t count_limit = 1;; count_limit *= 2) {
-    int n = 0;
-    for (int i = length - 1; i >= 0; --i) {
-      if (data[i]) keys[n++] = (static_cast<uint64_t>(std::max(data[i], count_limit)) << 16) | (0xffff - i);
-    }
-    if (n == 1) {
-      depth[0xffff - (keys[0] & 0xffff)] = 1;
-      break;
-    }
-    std::sort(keys, keys + n);
-    for (int k = 0; k < n; ++k)
+    // leaves with count <= count_limit: key (count_limit, symbol)
+    int low = 0;
+    while (low < n && (base[low] >> 16) <= count_limit) ++low;
+    for (int k = 0; k < low; ++k) keys[k] = (static_cast<uint64_t>(count_limit) << 16) | (base[k] & 0xffff);
+    std::sort(keys, keys + low);
+    std::copy(base + low, base + n, keys + low);
+    for (int k = 0; k < n; ++k) {
       tree[k] = TreeNode{static_cast<uint32_t>(keys[k] >> 16), -1,
                          static_cast<int16_t>(0xffff - (keys[k] & 0xffff))};
+      height[k] = 0;
+    }
     const TreeNode sentinel{~0u, -1, -1};
     tree[n] = sentinel;
     tree[n + 1] = sentinel;
@@ -190,9 +205,10 @@ void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t
       tree[parent].total = tree[left].total + tree[right].total;
       tree[parent].left = static_cast<int16_t>(left);
       tree[parent].right_or_value = static_cast<int16_t>(right);
+      height[parent] = static_cast<uint8_t>(1 + std::max(height[left], height[right]));
       tree[parent + 1] = sentinel;
     }
-    if (AssignDepths(2 * n - 1, tree, depth, max_depth)) break;
+    if (height[2 * n - 1] <= max_depth && AssignDepths(2 * n - 1, tree, depth, max_depth)) break;
   }
 }
 

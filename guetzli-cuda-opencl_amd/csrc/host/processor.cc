@@ -200,6 +200,49 @@ int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram
   return ncomp;
 }
 
+namespace {
+// Staged histograms (6 x 256 counts, chroma non-zero count) -> per-component
+// DC / AC histograms as SaveToJpegData stores them; returns the component
+// count.
+int HistogramsFromStage(const uint32_t* hist, uint64_t chroma, JpegHistogram dc[3],
+                        JpegHistogram ac[3]) {
+  const int ncomp = chroma > 0 ? 3 : 1;  // SaveToJpegData drops all-zero chroma
+  for (int c = 0; c < 3; ++c) {
+    dc[c].Clear();
+    ac[c].Clear();
+    if (c >= ncomp) continue;
+    for (int i = 0; i < 256; ++i) {
+      dc[c].counts[i] = 2 * hist[(2 * c) * 256 + i];
+      ac[c].counts[i] = 2 * hist[(2 * c + 1) * 256 + i];
+    }
+  }
+  return ncomp;
+}
+
+// Headers (*prologue) and Huffman code tables of an image with these
+// histograms (WriteJpeg's table choice, jpeg_data_writer.cc).
+bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                 bool strip_metadata, int ncomp, JpegHistogram* dc_h, JpegHistogram* ac_h,
+                 std::string* prologue, JpegCodeTables* codes) {
+  JpegData hdr;
+  hdr.app_data = meta.app_data;
+  hdr.com_data = meta.com_data;
+  JpegHeaderFor(w, h, q, ncomp, &hdr);
+  HuffCodeTable dc_tab[3], ac_tab[3];
+  prologue->clear();
+  if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, prologue)) return false;
+  std::memset(codes, 0, sizeof(*codes));
+  for (int c = 0; c < ncomp; ++c)
+    for (int i = 0; i < 256; ++i) {
+      codes->dc_len[c][i] = dc_tab[c].depth[i];
+      codes->ac_len[c][i] = ac_tab[c].depth[i];
+      codes->dc_code[c][i] = static_cast<uint16_t>(dc_tab[c].code[i]);
+      codes->ac_code[c][i] = static_cast<uint16_t>(ac_tab[c].code[i]);
+    }
+  return true;
+}
+}  // namespace
+
 bool DeviceEncodeJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
                       bool strip_metadata, std::string* prologue, size_t* size, std::string* err) {
   JpegHistogram dc_h[3], ac_h[3];
@@ -269,6 +312,44 @@ bool HipButteraugliComparator::DeviceWriteJpeg(const CoeffImage& img, const Jpeg
                                                bool strip_metadata, std::string* out) {
   if (!SyncCoeffs(img)) return false;
   return gz::DeviceWriteJpeg(engine_.get(), w_, h_, img.quant, meta, strip_metadata, out, &err_);
+}
+
+bool HipButteraugliComparator::DeviceEncodeAndCompare(const CoeffImage& img,
+                                                      const JpegData& meta, bool strip_metadata,
+                                                      size_t* size) {
+  // One stream order: histogram stage, Compare pass, then the scan; the host
+  // builds the Huffman codes from the staged histograms while the Compare
+  // pass runs, and waits once for both results.
+  const auto t0 = Clock::now();
+  if (!SyncCoeffs(img)) return false;
+  Engine* e = engine_.get();
+  uint32_t hist[6 * 256];
+  uint64_t chroma = 0;
+  if (!e->JpegStageEnqueue(img.quant) || !e->CompareEnqueue() || !e->JpegStageWait(hist, &chroma)) {
+    err_ = e->error();
+    return false;
+  }
+  JpegHistogram dc_h[3], ac_h[3];
+  const int ncomp = HistogramsFromStage(hist, chroma, dc_h, ac_h);
+  JpegCodeTables codes;
+  if (!PrepareScan(w_, h_, img.quant, meta, strip_metadata, ncomp, dc_h, ac_h, &cur_prologue_,
+                   &codes)) {
+    err_ = "jpeg header";
+    return false;
+  }
+  seconds_encode += Since(t0);
+  uint64_t nbits = 0, ff = 0;
+  if (!e->JpegScanEnqueue(ncomp, codes) || !e->Sync() || !e->JpegScanFinish(&nbits, &ff)) {
+    err_ = e->error();
+    return false;
+  }
+  e->CompareFinish(&distance_, block_max_.data());
+  ++compares;
+  // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
+  cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
+  *size = cur_size_;
+  seconds_compare += Since(t0);
+  return true;
 }
 
 bool HipButteraugliComparator::DeviceEncode(const CoeffImage& img, const JpegData& meta,
@@ -370,35 +451,61 @@ void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int 
                                  double target_mul, int factor_x, int factor_y,
                                  const std::vector<float>& max_dist_per_block,
                                  std::vector<float>* block_weight) {
-  // butteraugli_comparator.cc:169-233 (block maxima come from the device)
+  // butteraugli_comparator.cc:169-233 (block maxima come from the device).
+  // Rows of blocks in parallel; the direction < 0 scatter of the reference
+  // (every over-target block raises its neighbours to 1 / (d + 1)) is formed
+  // as the equivalent gather -- a max over the same values, order-free.
   const double target_distance = target * target_mul;
   const int sizex = 8 * factor_x, sizey = 8 * factor_y;
   const int bw = (w + sizex - 1) / sizex, bh = (h + sizey - 1) / sizey;
-  for (int by = 0; by < bh; ++by) {
-    for (int bx = 0; bx < bw; ++bx) {
-      const int bix = by * bw + bx;
-      float max_local = static_cast<float>(target_distance);
-      const int x0 = std::max(0, bx - max_block_dist), y0 = std::max(0, by - max_block_dist);
-      const int x1 = std::min(bw, bx + 1 + max_block_dist), y1 = std::min(bh, by + 1 + max_block_dist);
-      for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) max_local = std::max(max_local, max_dist_per_block[y * bw + x]);
-      if (direction > 0) {
-        if (max_dist_per_block[bix] <= target_distance && max_local <= 1.1 * target_distance)
-          (*block_weight)[bix] = 1.0;
-      } else {
-        constexpr double kLocalMaxWeight = 0.5;
-        if (max_dist_per_block[bix] <=
-            (1 - kLocalMaxWeight) * target_distance + kLocalMaxWeight * max_local)
-          continue;
+  const int r = max_block_dist;
+  auto max_local = [&](int bx, int by) {
+    float m = static_cast<float>(target_distance);
+    const int x0 = std::max(0, bx - r), y0 = std::max(0, by - r);
+    const int x1 = std::min(bw, bx + 1 + r), y1 = std::min(bh, by + 1 + r);
+    for (int y = y0; y < y1; ++y)
+      for (int x = x0; x < x1; ++x) m = std::max(m, max_dist_per_block[y * bw + x]);
+    return m;
+  };
+  constexpr int kRows = 8;
+  const int chunks = (bh + kRows - 1) / kRows;
+  if (direction > 0) {
+    ParallelFor(chunks, [&](int ch) {
+      for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+        for (int bx = 0; bx < bw; ++bx) {
+          const int bix = by * bw + bx;
+          if (max_dist_per_block[bix] <= target_distance && max_local(bx, by) <= 1.1 * target_distance)
+            (*block_weight)[bix] = 1.0;
+        }
+    });
+    return;
+  }
+  constexpr double kLocalMaxWeight = 0.5;
+  std::vector<uint8_t> active(static_cast<size_t>(bw) * bh);
+  ParallelFor(chunks, [&](int ch) {
+    for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        const int bix = by * bw + bx;
+        active[bix] = !(max_dist_per_block[bix] <=
+                        (1 - kLocalMaxWeight) * target_distance + kLocalMaxWeight * max_local(bx, by));
+      }
+  });
+  ParallelFor(chunks, [&](int ch) {
+    for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        const int ix = by * bw + bx;
+        float wgt = (*block_weight)[ix];
+        const int x0 = std::max(0, bx - r), y0 = std::max(0, by - r);
+        const int x1 = std::min(bw, bx + 1 + r), y1 = std::min(bh, by + 1 + r);
         for (int y = y0; y < y1; ++y)
           for (int x = x0; x < x1; ++x) {
+            if (!active[y * bw + x]) continue;
             const int d = std::max(std::abs(y - by), std::abs(x - bx));
-            const int ix = y * bw + x;
-            (*block_weight)[ix] = std::max<float>((*block_weight)[ix], 1.0f / (d + 1.0f));
+            wgt = std::max<float>(wgt, 1.0f / (d + 1.0f));
           }
+        (*block_weight)[ix] = wgt;
       }
-    }
-  }
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -677,6 +784,25 @@ class Processor {
     res_->detail["write_stage_s"] += dt;
     return true;
   }
+  // BeginOutput(img) followed by the Compare of img; with a device writer
+  // both run as one overlapped device call (the candidate's size and its
+  // distance come back together).
+  bool EncodeAndCompare(const JpegData& jpg, const CoeffImage& img, std::string* err) {
+    if (!cmp_->HasDeviceWriter()) {
+      if (!BeginOutput(jpg, img, err)) return false;
+      return cmp_->Compare(img) || Fail(err);
+    }
+    FlushOutput();
+    const auto t0 = Clock::now();
+    size_t size = 0;
+    if (!cmp_->DeviceEncodeAndCompare(img, jpg, params_.clear_metadata, &size)) return Fail(err);
+    pending_.clear();
+    pending_size_ = size;
+    has_pending_ = true;
+    pending_device_ = true;
+    res_->detail["encode_compare_s"] += Since(t0);
+    return true;
+  }
   // Joins the pending encode and applies its MaybeOutput; returns its size.
   size_t FlushOutput() {
     if (!has_pending_) return 0;
@@ -752,9 +878,8 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
   const auto tq = Clock::now();
   if (!cmp_->QuantizeFromOriginal(q, img, /*need_host=*/!cmp_->HasDeviceWriter())) return Fail(err);
   res_->seconds_quantize += Since(tq);
-  if (!BeginOutput(jpg_in, *img, err)) return false;
   ++res_->iterations;
-  if (!cmp_->Compare(*img)) return Fail(err);
+  if (!EncodeAndCompare(jpg_in, *img, err)) return false;
   data->dist_ok = cmp_->DistanceOK(target_mul);
   data->jpg_size = FlushOutput();
   return true;
@@ -1083,8 +1208,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
-      if (!BeginOutput(jpg, *img, err)) return false;
-      if (!cmp_->Compare(*img)) return Fail(err);
+      if (!EncodeAndCompare(jpg, *img, err)) return false;
       prev_size = est_jpg_size;
     }
   }

@@ -68,6 +68,12 @@ class Comparator {
                             size_t* size) {
     return false;
   }
+  // DeviceEncode of img followed by Compare(img), for comparators that can
+  // overlap the two (the default runs them one after the other).
+  virtual bool DeviceEncodeAndCompare(const CoeffImage& img, const JpegData& meta,
+                                      bool strip_metadata, size_t* size) {
+    return DeviceEncode(img, meta, strip_metadata, size) && Compare(img);
+  }
   virtual void DeviceKeepEncoded() {}
   virtual bool DeviceFetchKept(std::string* out) { return false; }
   // DC / AC histograms of img as SaveToJpegData stores it (comps at or above
@@ -134,8 +140,11 @@ class HipButteraugliComparator : public Comparator {
                        std::string* out) override;
   bool DeviceEncode(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                     size_t* size) override;
+  bool DeviceEncodeAndCompare(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                              size_t* size) override;
   void DeviceKeepEncoded() override;
   bool DeviceFetchKept(std::string* out) override;
+  double seconds_encode = 0.0;  // host part of the overlapped encodes
   int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) override;
   double ScoreOutputSize(int size) const override;
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }

@@ -562,6 +562,7 @@ Engine::~Engine() {
   for (void* p : bufs)
     if (p) hipFree(p);
   if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
+  if (stage_event_) hipEventDestroy(static_cast<hipEvent_t>(stage_event_));
   if (h_block_max_) hipHostFree(h_block_max_);
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
   if (h_zero_off_) hipHostFree(h_zero_off_);
@@ -826,8 +827,22 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
 bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  if (dbg || g_prof_on.load()) {
+  if (dbg) {
     if (!EnqueueCompare(dbg)) return false;
+    GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
+  } else if (!CompareEnqueue()) {
+    return false;
+  }
+  if (!Sync()) return false;
+  CompareFinish(distance, block_max);
+  return true;
+}
+
+bool Engine::CompareEnqueue() {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (g_prof_on.load()) {
+    if (!EnqueueCompare(nullptr)) return false;
   } else {
     if (!compare_graph_) {
       hipGraph_t g = nullptr;
@@ -848,13 +863,20 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(compare_graph_), s));
   }
   GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::Sync() {
+  GZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream_)));
   ProfFlush();
+  return true;
+}
+
+void Engine::CompareFinish(float* distance, float* block_max) {
   float d = 0.0f;
   for (int b = 0; b < nb_; ++b) d = d < h_block_max_[b] ? h_block_max_[b] : d;
   if (block_max) memcpy(block_max, h_block_max_, nb_ * 4);
   *distance = d;
-  return true;
 }
 
 bool Engine::StartBlockComparisons(float* mask_scale_host) {
@@ -957,8 +979,17 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
 }
 
 bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) {
+  return JpegStageEnqueue(q) && JpegStageWait(hist, chroma_nz);
+}
+
+bool Engine::JpegStageEnqueue(const int q[3][64]) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  if (!stage_event_) {
+    hipEvent_t ev;
+    GZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    stage_event_ = ev;
+  }
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
@@ -967,8 +998,12 @@ bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) 
       d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_,
       reinterpret_cast<unsigned long long*>(d_jhist_ + 6 * 256)));
   GZ_HIP(hipMemcpyAsync(h_jhist_, d_jhist_, 6 * 256 * 4 + 8, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
-  ProfFlush();
+  GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
+  return true;
+}
+
+bool Engine::JpegStageWait(uint32_t* hist, uint64_t* chroma_nz) {
+  GZ_HIP(hipEventSynchronize(static_cast<hipEvent_t>(stage_event_)));
   memcpy(hist, h_jhist_, 6 * 256 * 4);
   uint64_t nz;
   memcpy(&nz, h_jhist_ + 6 * 256, 8);
@@ -977,11 +1012,17 @@ bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) 
 }
 
 bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff) {
+  // the pinned code staging may still feed the previous scan's copy
+  GZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream_)));
+  return JpegScanEnqueue(ncomp, codes) && Sync() && JpegScanFinish(nbits, ff);
+}
+
+// (the caller has synchronised since the previous scan: the pinned code
+// staging is free)
+bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
-  // the pinned code staging may still feed the previous scan's copy
-  GZ_HIP(hipStreamSynchronize(s));
   *h_jcodes_ = codes;
   GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodeTables), hipMemcpyHostToDevice, s));
   const JpegCodeTables* dc = static_cast<const JpegCodeTables*>(d_jcodes_);
@@ -995,8 +1036,10 @@ bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, u
                          k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_)));
   // (0xff count, bit total) in one read
   GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jinfo_, 8, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
-  ProfFlush();
+  return true;
+}
+
+bool Engine::JpegScanFinish(uint64_t* nbits, uint64_t* ff) {
   const uint64_t total = static_cast<uint32_t>(h_jhist_[6 * 256 + 3]);
   if ((total + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
   jnbits_[jslot_] = total;

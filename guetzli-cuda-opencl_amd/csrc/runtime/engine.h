@@ -110,6 +110,19 @@ class Engine {
   bool JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff);
   void JpegKeep() { jslot_ ^= 1; }
   bool JpegFetch(bool kept, const uint8_t** bytes, uint64_t* nbits);
+  // The same steps split for overlap within one stream order: *Enqueue
+  // queues work without waiting; JpegStageWait waits for the staged
+  // histograms only (an event), Sync for everything queued, after which
+  // CompareFinish / JpegScanFinish read the results.  The search runs
+  // stage -> Compare pass -> (host builds the codes while the pass runs)
+  // -> scan, with one full synchronisation per candidate.
+  bool JpegStageEnqueue(const int q[3][64]);
+  bool JpegStageWait(uint32_t* hist, uint64_t* chroma_nz);
+  bool CompareEnqueue();
+  bool JpegScanEnqueue(int ncomp, const JpegCodeTables& codes);
+  bool Sync();
+  void CompareFinish(float* distance, float* block_max);
+  bool JpegScanFinish(uint64_t* nbits, uint64_t* ff);
   bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
   bool OrderBlocks(int comp_mask);
 
@@ -133,6 +146,7 @@ class Engine {
   bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b);
   bool EnqueueCompare(CompareDebug* dbg);
   void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
+  void* stage_event_ = nullptr;    // hipEvent_t: the staged histograms reached the host
 
   int device_ = 0;
   int w_ = 0, h_ = 0, bw_ = 0, bh_ = 0, nb_ = 0, rw_ = 0, rh_ = 0;
