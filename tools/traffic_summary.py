@@ -47,7 +47,10 @@ def calibrate(d):
     write = load(d, "WRITE_SIZE")
     out = {"read": {}, "write": {}, "raw": {}}
     for k, vals in list(fetch.items()) + list(write.items()):
+        # "void k_read<HIP_vector_type<float, 2u> >(...)" -> "k_read<float2>"
         short = k.split("(")[0].replace("void ", "")
+        short = short.replace("HIP_vector_type<float, 2u> ", "float2")
+        short = short.replace("HIP_vector_type<float, 4u> ", "float4")
         name = short.split(" ")[-1]
         for key, b in known.items():
             if key.replace("<", "").replace(">", "") == name.replace("<", "").replace(">", ""):
