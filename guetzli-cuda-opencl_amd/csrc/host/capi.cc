@@ -38,6 +38,7 @@ struct gz_comparator {
   float distance = 0.0f;
   int w = 0, h = 0;
   std::vector<float> block_max;
+  std::vector<int16_t> last;  // coefficients of the last compare (distmap())
 };
 
 extern "C" {
@@ -96,6 +97,7 @@ static gz_status CompareImpl(gz_comparator* cmp, const int16_t* coeffs, gz::Comp
   cmp->block_max.resize(e.blocks());
   if (!e.UploadCoeffs(coeffs) || !e.Compare(&cmp->distance, cmp->block_max.data(), dbg))
     return SetError(GZ_ERR_DEVICE, "compare: " + e.error());
+  cmp->last.assign(coeffs, coeffs + static_cast<size_t>(e.blocks()) * 192);
   if (distance) *distance = cmp->distance;
   return GZ_OK;
 }
@@ -122,6 +124,33 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
     dbg.distmap = st->distmap;
   }
   return CompareImpl(cmp, coeffs, &dbg, distance);
+}
+
+gz_status gz_comparator_distmap(gz_comparator* cmp, float* out) {
+  if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "distmap: bad argument");
+  if (cmp->last.empty()) return SetError(GZ_ERR_INVALID_ARG, "distmap: no compare yet");
+  gz::Engine& e = *cmp->engine;
+  // the pass again on the same candidate, with the map read back (the
+  // search's passes keep only the per-block maxima)
+  gz::CompareDebug dbg;
+  dbg.distmap = out;
+  float d = 0.0f;
+  if (!e.UploadCoeffs(cmp->last.data()) || !e.Compare(&d, nullptr, &dbg))
+    return SetError(GZ_ERR_DEVICE, "distmap: " + e.error());
+  return GZ_OK;
+}
+
+gz_status gz_comparator_compare_blocks(gz_comparator* cmp, int n, const int* blocks,
+                                       const int16_t* cand, double* err) {
+  if (!cmp || n < 0 || (n > 0 && (!blocks || !cand || !err)))
+    return SetError(GZ_ERR_INVALID_ARG, "compare_blocks: bad argument");
+  gz::Engine& e = *cmp->engine;
+  for (int i = 0; i < n; ++i)
+    if (blocks[i] < 0 || blocks[i] >= e.blocks())
+      return SetError(GZ_ERR_INVALID_ARG, "compare_blocks: block index out of range");
+  if (!e.CompareBlocks(n, blocks, cand, err))
+    return SetError(GZ_ERR_DEVICE, "compare_blocks: " + e.error());
+  return GZ_OK;
 }
 
 gz_status gz_comparator_original_coeffs(gz_comparator* cmp, int16_t* out) {

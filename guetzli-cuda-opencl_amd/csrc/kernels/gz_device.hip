@@ -558,7 +558,7 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
                   d_delta_val_, d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
@@ -892,6 +892,38 @@ bool Engine::StartBlockComparisons(float* mask_scale_host) {
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
   have_mask_scale_ = true;
+  return true;
+}
+
+bool Engine::CompareBlocks(int n, const int* blocks, const int16_t* cand, double* err) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (n <= 0) return true;
+  for (int i = 0; i < n; ++i)
+    if (blocks[i] < 0 || blocks[i] >= nb_) return Fail("CompareBlocks block index", 0);
+  if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  // one staging buffer: block indices | candidates | errors
+  const size_t need = static_cast<size_t>(n) * (4 + 192 * 2 + 8) + 64;
+  if (need > cbreq_cap_) {
+    GZ_HIP(hipStreamSynchronize(s));
+    if (d_cbreq_) GZ_HIP(hipFree(d_cbreq_));
+    d_cbreq_ = nullptr;
+    cbreq_cap_ = 0;
+    GZ_HIP(hipMalloc(&d_cbreq_, need));
+    cbreq_cap_ = need;
+  }
+  char* base = static_cast<char*>(d_cbreq_);
+  int* d_blocks = reinterpret_cast<int*>(base);
+  int16_t* d_cand = reinterpret_cast<int16_t*>(base + ((static_cast<size_t>(n) * 4 + 15) & ~15ull));
+  double* d_err = reinterpret_cast<double*>(
+      reinterpret_cast<char*>(d_cand) + ((static_cast<size_t>(n) * 384 + 15) & ~15ull));
+  GZ_HIP(hipMemcpyAsync(d_blocks, blocks, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_cand, cand, static_cast<size_t>(n) * 384, hipMemcpyHostToDevice, s));
+  GZ_TIMED("compare_blocks", k_compare_blocks<<<n, 64, 0, s>>>(d_blocks, d_cand, n, d_rgb_, d_mask_scale_,
+                                                                w_, h_, bw_, d_err));
+  GZ_HIP(hipMemcpyAsync(err, d_err, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
   return true;
 }
 

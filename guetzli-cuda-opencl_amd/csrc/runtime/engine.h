@@ -96,6 +96,10 @@ class Engine {
   bool BlockZeroingCandidates(int comp_mask, float limit, int lookahead, bool new_model,
                               std::vector<int>* offsets,
                               std::vector<uint8_t>* idx, std::vector<float>* err);
+  // SwitchBlock + CompareBlock for n (block, candidate [3][64]) requests;
+  // err[i] receives CompareBlock's double (the comparator-level adapter's
+  // per-block entry; the search itself uses the batched calls above).
+  bool CompareBlocks(int n, const int* blocks, const int16_t* cand, double* err);
 
   // Device entropy coding of the current coefficients with quant q (the
   // per-iteration JPEG of the search).  JpegStage: quantized zigzag
@@ -212,6 +216,8 @@ class Engine {
   uint32_t* h_delta_idx_ = nullptr;   // ... (pinned host)
   int16_t* h_delta_val_ = nullptr;
   size_t delta_cap_ = 0;
+  void* d_cbreq_ = nullptr;  // CompareBlocks staging (indices | candidates | errors)
+  size_t cbreq_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
   float* h_block_max_ = nullptr;

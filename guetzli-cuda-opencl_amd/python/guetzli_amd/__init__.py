@@ -77,7 +77,8 @@ EXPORTED_SYMBOLS = (
     "gz_comparator_original_coeffs", "gz_comparator_write_jpeg", "gz_write_jpeg_host",
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
-    "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode",
+    "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode", "gz_comparator_distmap",
+    "gz_comparator_compare_blocks",
 )
 
 _lib = None
@@ -128,6 +129,10 @@ def lib():
     L.gz_comparator_compare.restype = i32
     L.gz_comparator_compare_stages.argtypes = [vp, vp, ctypes.POINTER(_Stages), ctypes.POINTER(f32)]
     L.gz_comparator_compare_stages.restype = i32
+    L.gz_comparator_distmap.argtypes = [vp, vp]
+    L.gz_comparator_distmap.restype = i32
+    L.gz_comparator_compare_blocks.argtypes = [vp, i32, vp, vp, vp]
+    L.gz_comparator_compare_blocks.restype = i32
     L.gz_comparator_block_max.argtypes = [vp, vp]
     L.gz_comparator_block_max.restype = i32
     L.gz_comparator_distance_ok.argtypes = [vp, ctypes.c_double]
@@ -555,6 +560,26 @@ class ButteraugliComparator:
                "compare_stages")
         arrs["distance"] = d.value
         return arrs
+
+    def distmap(self):
+        """Comparator::distmap() of the last compare (h x w floats)."""
+        out = np.zeros(self.width * self.height, dtype=np.float32)
+        _check(lib().gz_comparator_distmap(self._h, _ptr(out)), "distmap")
+        return out.reshape(self.height, self.width)
+
+    def compare_blocks(self, blocks, candidates):
+        """SwitchBlock + CompareBlock (butteraugli_comparator.cc:85-163) per
+        request: block indices (n,) and candidate coefficients (n, 3, 64);
+        returns CompareBlock's doubles."""
+        b = np.ascontiguousarray(blocks, dtype=np.int32).reshape(-1)
+        c = np.ascontiguousarray(candidates, dtype=np.int16).reshape(-1)
+        if c.size != 192 * b.size:
+            raise GuetzliError(1, "compare_blocks: %d candidates for %d blocks" % (c.size // 192,
+                                                                                   b.size))
+        err = np.zeros(b.size, dtype=np.float64)
+        _check(lib().gz_comparator_compare_blocks(self._h, b.size, _ptr(b), _ptr(c), _ptr(err)),
+               "compare_blocks")
+        return err
 
     def block_max(self):
         out = np.zeros(self.blocks, dtype=np.float32)

@@ -172,6 +172,10 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
  * integer FDCT + q=1 quantizer (guetzli/jpeg_data_encoder.cc:66-136,
  * guetzli/fdct.cc). */
 gz_status gz_comparator_original_coeffs(gz_comparator* cmp, int16_t* out);
+/* Comparator::distmap() (comparator.h:71-75): the distance map of the last
+ * gz_comparator_compare (w*h floats; recomputed on the device from the same
+ * candidate -- the search's own passes keep only per-block maxima). */
+gz_status gz_comparator_distmap(gz_comparator* cmp, float* out);
 /* Per-8x8-block maxima of the last distance map (ceil(w/8)*ceil(h/8)). */
 gz_status gz_comparator_block_max(gz_comparator* cmp, float* out);
 /* ComputeBlockErrorAdjustmentWeights (butteraugli_comparator.cc:169-233) on
@@ -202,6 +206,19 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
                                              const int16_t* orig_coeffs, int comp_mask,
                                              float limit, int lookahead, int new_zeroing_model,
                                              gz_coeff_data* out);
+
+/* SwitchBlock(bx, by, 1, 1) + CompareBlock(img, 0, 0, candidate, comp_mask)
+ * (butteraugli_comparator.cc:85-163) for n requests at once: request i
+ * compares 8x8 block blocks[i] (row-major block index) of the reference image
+ * with candidate coefficients cand[192*i ..] -- [3][64], natural order,
+ * dequantized, every component as the image holds it (the masked
+ * components' candidate values, the image's current values for the others)
+ * -- and err[i] receives CompareBlock's double.  Uses the activity mask of
+ * StartBlockComparisons (run first if needed).  The per-block entry of the
+ * comparator-level drop-in; the search itself uses the
+ * batched gz_comparator_block_zeroing_orders. */
+gz_status gz_comparator_compare_blocks(gz_comparator* cmp, int n, const int* blocks,
+                                       const int16_t* cand, double* err);
 
 /* SaveToJpegData + WriteJpeg (guetzli/output_image.cc:579-640,
  * jpeg_data_writer.cc:540-553) of dequantized coefficients `coeffs`

@@ -1180,6 +1180,23 @@ static double compare_block(const float* rgb0_c, const float* cand_lin, const fl
   return sqrt((1 - kEdgeWeight) * diff + kEdgeWeight * diff_edge);
 }
 
+/* SwitchBlock(bx, by, 1, 1) + CompareBlock (butteraugli_comparator.cc:85-163)
+ * of block `bix` with candidate coefficients block[3][64]. */
+double gzo_compare_block(int w, int h, const uint8_t* ref_rgb, const float* ref_mask, int bix,
+                         const int16_t* block) {
+  gzo_init();
+  const int bw = (w + 7) / 8, bx = bix % bw, by = bix / bw;
+  const size_t n = (size_t)w * h;
+  float rgb0_c[192];
+  block_linear(w, h, ref_rgb, bx, by, rgb0_c);
+  gzo_opsin_dynamics(8, 8, rgb0_c);
+  const size_t corner = (size_t)(8 * by) * w + 8 * bx;
+  const float scale[3] = {ref_mask[corner], ref_mask[n + corner], ref_mask[2 * n + corner]};
+  float lin[192];
+  candidate_linear(w, h, bx, by, block, lin);
+  return compare_block(rgb0_c, lin, scale);
+}
+
 void gzo_block_zeroing_orders(int w, int h, const uint8_t* ref_rgb, const float* ref_mask,
                               const int16_t* cur_coeffs, const int16_t* orig_coeffs,
                               float limit, int lookahead, int comp_mask, int new_model,

@@ -86,6 +86,12 @@ void gzo_block_diff_double(double* xyb0, double* xyb1, double dc[3], double ac[3
  * exact (unstable) tie order: introsort + final insertion sort. */
 void gzo_sort_pairs(int* idx, float* key, int n);
 
+/* SwitchBlock(bx, by, 1, 1) + CompareBlock (butteraugli_comparator.cc:85-163)
+ * of 8x8 block `bix` with candidate coefficients block[3][64] (ref_mask as
+ * below); returns CompareBlock's double. */
+double gzo_compare_block(int w, int h, const uint8_t* ref_rgb, const float* ref_mask, int bix,
+                         const int16_t* block);
+
 /* Per-block greedy zeroing order of the CPU_OPT loop
  * (processor.cc:376-487, 641-672; butteraugli_comparator.cc:72-163).
  * ref_mask: MaskOpt(ref_xyb, ref_xyb).mask (3*w*h), i.e. mask_xyz_.

@@ -59,6 +59,8 @@ def lib():
         L.gzo_block_zeroing_orders.argtypes = [ctypes.c_int, ctypes.c_int, u8, f32, i16, i16,
                                                ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_void_p]
+        L.gzo_compare_block.argtypes = [ctypes.c_int, ctypes.c_int, u8, f32, ctypes.c_int, i16]
+        L.gzo_compare_block.restype = ctypes.c_double
         L.gzo_srgb8_to_linear.argtypes = [ctypes.c_int]
         L.gzo_srgb8_to_linear.restype = ctypes.c_double
         L.gzo_init()

@@ -93,6 +93,49 @@ def test_block_zeroing_orders_bit_exact(gz, case, variant):
 
 
 @pytest.mark.parametrize("case", fixture_cases())
+def test_compare_blocks_bit_exact(gz, case):
+    """SwitchBlock + CompareBlock (butteraugli_comparator.cc:85-163) through
+    gz_comparator_compare_blocks: every block with its current coefficients
+    and with one random non-zero coefficient zeroed equals the oracle's
+    double bit for bit (edge blocks included)."""
+    F = Fixture(case)
+    L = oracle()
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    cur = F.i16("cand_coeffs.i16").reshape(3, F.nb, 64)
+    mask = F.f32("ref_mask.f32")
+    rgb = np.ascontiguousarray(F.rgb(), dtype=np.uint8).ravel()
+    rng = np.random.default_rng(17)
+    blocks, cands = [], []
+    for b in range(F.nb):
+        blk = np.ascontiguousarray(cur[:, b, :]).copy()
+        blocks.append(b)
+        cands.append(blk.copy())
+        nz = np.flatnonzero(blk.reshape(-1))
+        if nz.size:
+            blk.reshape(-1)[rng.choice(nz)] = 0
+            blocks.append(b)
+            cands.append(blk)
+    cands = np.stack(cands).astype(np.int16)
+    err = cmp.compare_blocks(np.array(blocks), cands)
+    ref = np.array([L.gzo_compare_block(F.w, F.h, rgb, mask, b, np.ascontiguousarray(c).ravel())
+                    for b, c in zip(blocks, cands)], np.float64)
+    bad = np.flatnonzero(err.view(np.uint64) != ref.view(np.uint64))
+    assert bad.size == 0, "%d/%d differ, e.g. block %d: %r vs %r" % (
+        bad.size, err.size, blocks[bad[0]], err[bad[0]], ref[bad[0]])
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_comparator_distmap_bit_exact(gz, case):
+    """Comparator::distmap() after a Compare == the reference's map."""
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    d = cmp.compare(F.i16("cand_coeffs.i16"))
+    assert np.float32(d) == np.float32(F.meta["distance"])
+    ref = F.f32("distmap.f32")
+    assert bits_equal(cmp.distmap(), ref), mismatch(cmp.distmap(), ref)
+
+
+@pytest.mark.parametrize("case", fixture_cases())
 def test_device_fdct_matches_reference(gz, case):
     """EncodeRGBToJpeg's q=1 coefficients computed by the device kernel equal
     the reference's (fixture orig_coeffs)."""
