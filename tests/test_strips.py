@@ -172,7 +172,10 @@ def _gpu_strip_rank(rank, world, port, e, q):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
                             world_size=world)
     try:
-        rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+        if "seed" in e:
+            rgb = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+        else:
+            rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
         coll = gz.Collectives.from_torch(dist, "cpu")
         data = gz.process_strips(rgb, e["w"], e["h"], coll, gz.Params.for_quality(e["quality"]),
                                  device=0)
@@ -184,19 +187,21 @@ def _gpu_strip_rank(rank, world, port, e, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,world", [("bees_q95", 1), ("bees_q90", 2)])
+@pytest.mark.parametrize("name,world", [("bees_q95", 1), ("bees_q90", 2),
+                                        ("synth_8192x8192_s0_q84", 4)])
 def test_gpu_strips_reproduce_reference(name, world):
     """`world` ranks, each a process with its strip's engine on cuda:0, the
-    exchange over gloo: every rank returns the reference bytes."""
+    exchange over gloo: every rank returns the reference bytes -- including
+    BASELINE configs[4] (8192x8192 q84 as 4 strips of 2048 rows + halo)."""
     import torch.multiprocessing as mp
-    e = MANIFEST["e2e"][name]
+    e = MANIFEST["e2e"].get(name) or MANIFEST["synthetic"][name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_gpu_strip_rank, args=(r, world, port, e, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = dict(q.get(timeout=600) for _ in procs)
     for p in procs:
         p.join(60)
-    assert all(v == e["sha256"] for v in res.values()), res
+    assert len(res) == world and all(v == e["sha256"] for v in res.values()), res
