@@ -541,6 +541,7 @@ def main():
         "blur_mask_pass": blur_mask,
         "stages": stages,
         "gpu_ms_per_frame_isolated": round(gpu_frame_ms, 3),
+        "gpu_regions_ms_per_frame": {n: round(ms, 4) for ms, n, _ in regions},
         "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
         "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
         "host_cores_busy_per_gpu": round(cpu_s / elapsed, 2),

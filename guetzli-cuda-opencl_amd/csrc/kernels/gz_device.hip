@@ -451,9 +451,14 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jwords_[1]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jinfo_), 16);
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 16) != hipSuccess)
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 16, hipHostMallocCoherent) != hipSuccess)
+    ok = false;
+  if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_jhist_), e->h_jhist_, 0) != hipSuccess)
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodeTables)) != hipSuccess)
+    ok = false;
+  if (ok && (hipMemsetAsync(e->d_jhist_, 0, 6 * 256 * 4 + 16, s) != hipSuccess ||
+             hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess))
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
@@ -555,8 +560,8 @@ Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
-                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_, d_delta_idx_,
-                  d_delta_val_, d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
+                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
+                  d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_cbreq_};
   for (void* p : bufs)
@@ -626,33 +631,26 @@ bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n)
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (n == 0) return true;
+  // the previous delta's kernel may still read the pinned staging
+  GZ_HIP(hipStreamSynchronize(s));
   if (n > delta_cap_) {
-    // the previous staging buffers may still feed an in-flight copy
-    GZ_HIP(hipStreamSynchronize(s));
-    if (d_delta_idx_) GZ_HIP(hipFree(d_delta_idx_));
-    if (d_delta_val_) GZ_HIP(hipFree(d_delta_val_));
     if (h_delta_idx_) GZ_HIP(hipHostFree(h_delta_idx_));
     if (h_delta_val_) GZ_HIP(hipHostFree(h_delta_val_));
-    d_delta_idx_ = nullptr;
-    d_delta_val_ = nullptr;
     h_delta_idx_ = nullptr;
     h_delta_val_ = nullptr;
     delta_cap_ = 0;
     const size_t cap = std::max<size_t>(n + n / 2, 1 << 16);
-    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_delta_idx_), cap * 4));
-    GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_delta_val_), cap * 2));
-    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_idx_), cap * 4));
-    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_val_), cap * 2));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_idx_), cap * 4, hipHostMallocCoherent));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_delta_val_), cap * 2, hipHostMallocCoherent));
+    GZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_delta_idx_), h_delta_idx_, 0));
+    GZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_delta_val_), h_delta_val_, 0));
     delta_cap_ = cap;
-  } else {
-    // the pinned staging of the previous delta must have been consumed
-    GZ_HIP(hipStreamSynchronize(s));
   }
   memcpy(h_delta_idx_, idx, n * 4);
   memcpy(h_delta_val_, val, n * 2);
-  GZ_HIP(hipMemcpyAsync(d_delta_idx_, h_delta_idx_, n * 4, hipMemcpyHostToDevice, s));
-  GZ_HIP(hipMemcpyAsync(d_delta_val_, h_delta_val_, n * 2, hipMemcpyHostToDevice, s));
-  GZ_TIMED("scatter_coeffs", k_scatter_coeffs<<<(n + 255) / 256, 256, 0, s>>>(d_delta_idx_, d_delta_val_, n, d_cur_));
+  // the kernel reads the (index, value) pairs straight from pinned host
+  // memory: no staging copies in the stream
+  GZ_TIMED("scatter_coeffs", k_scatter_coeffs<<<(n + 255) / 256, 256, 0, s>>>(m_delta_idx_, m_delta_val_, n, d_cur_));
   return true;
 }
 
@@ -1025,11 +1023,10 @@ bool Engine::JpegStageEnqueue(const int q[3][64]) {
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
-  GZ_HIP(hipMemsetAsync(d_jhist_, 0, 6 * 256 * 4 + 16, s));
+  // (the device counts are zero: cleared at creation, and by the last
+  // workgroup of every stage after it has published them to h_jhist_)
   GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * nb_ + 255) / 256, 256, 0, s>>>(
-      d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_,
-      reinterpret_cast<unsigned long long*>(d_jhist_ + 6 * 256)));
-  GZ_HIP(hipMemcpyAsync(h_jhist_, d_jhist_, 6 * 256 * 4 + 8, hipMemcpyDeviceToHost, s));
+      d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;
 }
@@ -1065,9 +1062,9 @@ bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
   // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any scan)
   GZ_TIMED("jpeg_emit", (k_zero_words<<<512, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_),
                          k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
-                         k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_)));
-  // (0xff count, bit total) in one read
-  GZ_HIP(hipMemcpyAsync(h_jhist_ + 6 * 256 + 2, d_jinfo_, 8, hipMemcpyDeviceToHost, s));
+                         k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_,
+                                                              m_jhist_ + 6 * 256 + 2)));
+  // (0xff count, bit total) reach h_jhist_[1538..1539] from the last workgroup
   return true;
 }
 

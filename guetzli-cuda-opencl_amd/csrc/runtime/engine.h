@@ -193,16 +193,17 @@ class Engine {
   int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
   int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
   uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
-  uint32_t* d_jhist_ = nullptr;    //   6 x 256 counts + chroma non-zeros (u64)
+  uint32_t* d_jhist_ = nullptr;    //   6 x 256 counts + chroma non-zeros (u64) + done counter
   void* d_jcodes_ = nullptr;       //   JpegCodeTables
   int* d_jbitlen_ = nullptr;       //   [blocks]
   int* d_jbitoff_ = nullptr;       //   [blocks + 1]
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
   int jslot_ = 0;                  // current slot (kept = jslot_ ^ 1)
-  int* d_jinfo_ = nullptr;         //   0xff count
+  int* d_jinfo_ = nullptr;         //   0xff count, bit total, done counter
   size_t jwords_cap_ = 0;
-  uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + total bits
+  uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + (0xff count, total bits),
+  uint32_t* m_jhist_ = nullptr;    //   written by the kernels through this mapped address
   JpegCodeTables* h_jcodes_ = nullptr;
   uint8_t* h_jbytes_ = nullptr;
   size_t h_jbytes_cap_ = 0;
@@ -211,10 +212,10 @@ class Engine {
   float* h_cand_err_ = nullptr;
   size_t h_cand_cap_ = 0;
   float* d_scales_ = nullptr;  // [sigma][axis][scale_stride_] border scales
-  uint32_t* d_delta_idx_ = nullptr;   // UploadCoeffDelta staging (device)
-  int16_t* d_delta_val_ = nullptr;
-  uint32_t* h_delta_idx_ = nullptr;   // ... (pinned host)
+  uint32_t* h_delta_idx_ = nullptr;   // UploadCoeffDelta staging (pinned host)
   int16_t* h_delta_val_ = nullptr;
+  uint32_t* m_delta_idx_ = nullptr;   // ... their device-side (mapped) addresses
+  int16_t* m_delta_val_ = nullptr;
   size_t delta_cap_ = 0;
   void* d_cbreq_ = nullptr;  // CompareBlocks staging (indices | candidates | errors)
   size_t cbreq_cap_ = 0;
