@@ -64,6 +64,7 @@ def stage_bytes_per_px():
     s["coeffs_to_linear"] = 3 * 2 + 3 * 4          # int16 coeffs -> 3 f32 planes
     s["opsin_mhic"] = 3 * 4 + 3 * 4 + 6 * 4          # S1-S3 fused: linear + ref XYB -> m0, m1
     s["edge_blur"] = 6 * 4 + 6 * 4                  # S4: 6 separable blurs, 6 -> 6
+    s["edge_mask"] = 6 * 4 + 6 * 4 + 3 * 4          # S4 + S9-S11 fused: 6 -> 6 blurred + 3 mask front
     s["edge_map"] = 6 * 4 + 3 * 4 / 9.0
     s["block_diff"] = 6 * 4 + 6 * 4 / 9.0
     s["lowfreq_blur_h"] = 6 * 4 + 6 * 4 / 4.0
@@ -99,8 +100,8 @@ def region_bytes(name, w, h):
 # those stages (the opsin kernel also does the S2 transform and S3, combine the S13 LUTs with
 # S14/S15) are timed whole, so the extra fused work only lowers the figure.
 BLUR_MASK_BYTES_PER_PX = 272.0
-BLUR_MASK_STAGES = ("opsin_mhic", "edge_blur", "lowfreq_blur_h",
-                    "lowfreq_blur_v", "mask_front", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
+BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "lowfreq_blur_h",
+                    "lowfreq_blur_v", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
@@ -109,7 +110,7 @@ STAGE_SYMBOL = {
     "edge_blur": "void gz::k_blur_stream<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
     "lowfreq_blur_v": "void gz::k_blur_vstream<3>(", "low_freq": "gz::k_low_freq(",
-    "mask_front": "gz::k_mask_stream(",
+    "mask_front": "gz::k_mask_stream(", "edge_mask": "gz::k_edge_mask_stream(",
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
     "block_zeroing": "gz::k_block_zeroing(",

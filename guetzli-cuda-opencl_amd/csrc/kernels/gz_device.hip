@@ -670,9 +670,9 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   return true;
 }
 
-bool Engine::MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b) {
+bool Engine::MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b, bool front) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  {
+  if (front) {
     const int strips = (w_ + kMsCols - 1) / kMsCols, segs = (h_ + kMsRows - 1) / kMsRows;
     const int waves = 3 * strips * segs;
     GZ_TIMED("mask_front", k_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(xyb0, xyb1, w_, h_, strips, segs,
@@ -731,25 +731,15 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   }
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
   if (dbg && !d2h(dbg->mhic1, d_m1_, 3 * n)) return false;
-  // S4/S5: edge detector map (6 step-1 blurs of radius <= 3, fused 2-D)
+  // S4 + S9-S11: the edge detector's 6 step-1 blurs (radius <= 3) and the
+  // mask front, fused (one read of m0 / m1): blurred planes -> d_bl_, mask
+  // front -> d_mb_ (consumed by the mask blurs below)
   {
-    Blur2DPlanes b2{};
-    for (int c = 0; c < 3; ++c) {
-      const int sig = kSigEdgeX + c;
-      b2.in[c] = d_m0_ + c * n;
-      b2.in[3 + c] = d_m1_ + c * n;
-      b2.out[c] = d_bl_ + c * n;
-      b2.out[3 + c] = d_bl_ + (3 + c) * n;
-      b2.sig[c] = sig;
-      b2.sig[3 + c] = sig;
-    }
-    b2.nplanes = 6;
-    const int rows = kBsRows;
-    b2.tiles_x = (w_ + kBsCols - 1) / kBsCols;
-    b2.tiles_y = (h_ + rows - 1) / rows;
-    const int waves = b2.nplanes * b2.tiles_x * b2.tiles_y;
-    GZ_TIMED("edge_blur", k_blur_stream<kBlurEdge><<<(waves + 3) / 4, 256, 0, s>>>(
-        b2, w_, h_, rows, d_scales_, scale_stride_));
+    const int rows = EdgeMaskRows(w_, h_);
+    const int strips = (w_ + kEmCols - 1) / kEmCols, segs = (h_ + rows - 1) / rows;
+    const int waves = 3 * strips * segs;
+    GZ_TIMED("edge_mask", k_edge_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(
+        d_m0_, d_m1_, w_, h_, strips, segs, rows, d_bl_, d_mb_, d_scales_, scale_stride_));
   }
   GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
@@ -786,7 +776,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // the full B mask only for the stage dumps; Compare itself samples it at
   // (3j + 3, 3i + 3) alone
   const bool full_mask = dbg && (dbg->mask || dbg->mask_dc);
-  if (!MaskPipeline(d_m0_, d_m1_, !full_mask)) return false;
+  if (!MaskPipeline(d_m0_, d_m1_, !full_mask, false)) return false;  // front: edge_mask
   MaskPlanes mk = MaskPlanesOf(d_ma_, n, !full_mask);
   if (dbg && (dbg->mask || dbg->mask_dc)) {
     GZ_TIMED("mask_full_dbg", k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_));

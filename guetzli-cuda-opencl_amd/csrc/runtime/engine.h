@@ -147,7 +147,9 @@ class Engine {
     void* stop;
   };
   std::vector<PendingEvent> pending_;
-  bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b);
+  // MaskOpt's chain into d_ma_ (front: the mask front from xyb0 / xyb1 into
+  // d_mb_ first; false when the Compare pass's fused edge_mask made it).
+  bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b, bool front = true);
   bool EnqueueCompare(CompareDebug* dbg);
   void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
   void* stage_event_ = nullptr;    // hipEvent_t: the staged histograms reached the host
