@@ -73,6 +73,8 @@ def stage_bytes_per_px():
     s["mask_front"] = 6 * 4 + 3 * 4                 # S9-S11 fused: 6 planes -> 3
     s["mask_blur_h"] = 3 * 4 + 4 * (1 / 3.0 + 1 / 4.0 + 1.0)
     s["mask_blur_v"] = 4 * (1 / 3.0 + 1 / 4.0 + 1.0) + 4 * (1 / 9.0 + 1 / 16.0 + 1.0)
+    s["blur_h"] = s["lowfreq_blur_h"] + s["mask_blur_h"]    # S7 + S12 h passes, one launch
+    s["blur_v"] = s["lowfreq_blur_v"] + s["mask_blur_v"]    # S7 + S12 v passes, one launch
     s["combine"] = (3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 4) / 9.0
     s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
     s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
@@ -100,8 +102,7 @@ def region_bytes(name, w, h):
 # those stages (the opsin kernel also does the S2 transform and S3, combine the S13 LUTs with
 # S14/S15) are timed whole, so the extra fused work only lowers the figure.
 BLUR_MASK_BYTES_PER_PX = 272.0
-BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "lowfreq_blur_h",
-                    "lowfreq_blur_v", "mask_blur_h", "mask_blur_v", "combine", "diffmap_blur_h",
+BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
@@ -111,6 +112,7 @@ STAGE_SYMBOL = {
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
     "lowfreq_blur_v": "void gz::k_blur_vstream<3>(", "low_freq": "gz::k_low_freq(",
     "mask_front": "gz::k_mask_stream(", "edge_mask": "gz::k_edge_mask_stream(",
+    "blur_h": "void gz::k_blur_h4<6,", "blur_v": "void gz::k_blur_vstream<6>(",
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
     "block_zeroing": "gz::k_block_zeroing(",

@@ -250,7 +250,7 @@ inline dim3 BlurH4Grid(int w, int h, int planes, BlurPlanes& bp) {
 }
 inline RowsPlain Rows(const BlurPlanes& bp, int w) {
   RowsPlain r{};
-  for (int p = 0; p < 6; ++p) r.in[p] = bp.in[p];
+  for (int p = 0; p < kMaxBlurPlanes; ++p) r.in[p] = bp.in[p];
   r.w = w;
   return r;
 }
@@ -748,35 +748,37 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
       d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_));
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
-  // S7/S8: low-frequency edge term (sigma 14, step 4)
-  BlurPlanes bp{};
-  for (int c = 0; c < 3; ++c) {
-    bp.in[c] = d_m0_ + c * n;
-    bp.in[3 + c] = d_m1_ + c * n;
-    bp.sig[c] = kSigLowFreq;
-    bp.sig[3 + c] = kSigLowFreq;
-  }
-  for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
-  const dim3 grid7 = BlurH4Grid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-  GZ_TIMED("lowfreq_blur_h", k_blur_h4<kBlurLowFreq><<<grid7, 256, 0, s>>>(
-      Rows(bp, w_), bp, w_, h_, d_scales_, scale_stride_));
+  // S7 + S12: the six sigma-14 blurs (low-frequency edge term, m0 / m1) and
+  // the three mask blurs (of the mask front in d_mb_) as one horizontal and
+  // one vertical launch over nine planes; then S8.  The full B mask only for
+  // the stage dumps: Compare itself samples it at (3j + 3, 3i + 3) alone.
+  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc);
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
-    for (int p = 0; p < 6; ++p) {
-      bp.in[p] = d_tmp_ + p * n;
-      bp.out[p] = d_bl_ + p * dn;
+    BlurPlanes bp{};
+    for (int c = 0; c < 3; ++c) {
+      bp.in[c] = d_m0_ + c * n;
+      bp.in[3 + c] = d_m1_ + c * n;
+      bp.in[6 + c] = d_mb_ + c * n;
+      bp.sig[c] = bp.sig[3 + c] = kSigLowFreq;
+      bp.sig[6 + c] = c == 2 && !full_mask ? kSigMaskBSub : kSigMaskX + c;
     }
-    const dim3 grid8 = BlurVStreamGrid(w_, h_, 6, bp);  // fills bp's packed-grid fields
-    GZ_TIMED("lowfreq_blur_v", k_blur_vstream<kBlurLowFreq><<<grid8, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
+    // horizontal outputs: sigma-14 planes in d_tmp_, mask planes in d_xyb_
+    // (free after the opsin stage)
+    for (int p = 0; p < 6; ++p) bp.out[p] = d_tmp_ + p * n;
+    for (int c = 0; c < 3; ++c) bp.out[6 + c] = d_xyb_ + c * n;
+    const dim3 gh = BlurH4Grid(w_, h_, 9, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("blur_h", k_blur_h4<kBlurLfMask><<<gh, 256, 0, s>>>(Rows(bp, w_), bp, w_, h_, d_scales_,
+                                                                   scale_stride_));
+    for (int p = 0; p < 9; ++p) bp.in[p] = bp.out[p];
+    for (int p = 0; p < 6; ++p) bp.out[p] = d_bl_ + p * dn;
+    for (int c = 0; c < 3; ++c) bp.out[6 + c] = d_ma_ + c * n;
+    const dim3 gv = BlurVStreamGrid(w_, h_, 9, bp);  // fills bp's packed-grid fields
+    GZ_TIMED("blur_v", k_blur_vstream<kBlurLfMask><<<gv, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
-  // S9-S13: activity mask
-  // the full B mask only for the stage dumps; Compare itself samples it at
-  // (3j + 3, 3i + 3) alone
-  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc);
-  if (!MaskPipeline(d_m0_, d_m1_, !full_mask, false)) return false;  // front: edge_mask
   MaskPlanes mk = MaskPlanesOf(d_ma_, n, !full_mask);
   if (dbg && (dbg->mask || dbg->mask_dc)) {
     GZ_TIMED("mask_full_dbg", k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_));

@@ -98,15 +98,16 @@ struct GzTables {
 };
 
 // Planes handled by one launch of the separable blur (blockIdx.z = plane).
+constexpr int kMaxBlurPlanes = 9;  // the merged sigma-14 + mask launches
 struct BlurPlanes {
-  const float* in[6];
-  float* out[6];
-  int sig[6];
+  const float* in[kMaxBlurPlanes];
+  float* out[kMaxBlurPlanes];
+  int sig[kMaxBlurPlanes];
   // packed 1-D grid over the planes' (tile, row) work items: plane p owns
   // workgroups [start[p], start[p+1]), tiles[p] 256-wide tiles per row
   int nplanes;
-  int tiles[6];
-  int start[7];
+  int tiles[kMaxBlurPlanes];
+  int start[kMaxBlurPlanes + 1];
 };
 
 // Defined once in gz_device.hip (the single device translation unit).
