@@ -74,8 +74,11 @@ def stage_bytes_per_px():
     s["mask_blur_h"] = 3 * 4 + 4 * (1 / 3.0 + 1 / 4.0 + 1.0)
     s["mask_blur_v"] = 4 * (1 / 3.0 + 1 / 4.0 + 1.0) + 4 * (1 / 9.0 + 1 / 16.0 + 1.0)
     s["blur_h"] = s["lowfreq_blur_h"] + s["mask_blur_h"]    # S7 + S12 h passes, one launch
-    s["blur_v"] = s["lowfreq_blur_v"] + s["mask_blur_v"]    # S7 + S12 v passes, one launch
+    # S7 + S12 v passes in one launch, with S13 (the mask LUT pair of every
+    # blurred mask sample: one more decimated plane per channel)
+    s["blur_v"] = s["lowfreq_blur_v"] + s["mask_blur_v"] + 4 * (1 / 9.0 + 1 / 16.0 + 1 / 9.0)
     s["combine"] = (3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 4) / 9.0
+    s["combine_channels"] = (6 * 4 + 9 * 4 + 4) / 9.0    # S14/S15: LUT'd mask samples + dc/ac/edge -> R
     s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
     s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
     s["diffmap_final"] = 4 / 9.0 + 4 / 4.0 + 4 / 64.0
@@ -99,8 +102,11 @@ def region_bytes(name, w, h):
 
 # The "blur+mask pass" of BASELINE.json / SURVEY.md 8(d): blurs S1, S4, S7,
 # S16 and the mask chain S9-S13, 272 algorithmic B/px.  Kernels that carry
-# those stages (the opsin kernel also does the S2 transform and S3, combine the S13 LUTs with
-# S14/S15) are timed whole, so the extra fused work only lowers the figure.
+# those stages are timed whole (the opsin kernel also does the S2 transform
+# and S3, edge_mask also the S4 blurs, blur_v the S13 LUTs), so the extra
+# fused work only lowers the figure.  ("combine" carries S13 only in the
+# stage-dump path; the search's passes run S14/S15 alone as combine_channels,
+# which is outside the pass.)
 BLUR_MASK_BYTES_PER_PX = 272.0
 BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "diffmap_blur_h",
                     "diffmap_blur_v")
@@ -115,6 +121,7 @@ STAGE_SYMBOL = {
     "blur_h": "void gz::k_blur_h4<6,", "blur_v": "void gz::k_blur_vstream<6>(",
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
+    "combine_channels": "gz::k_combine_channels(",
     "block_zeroing": "gz::k_block_zeroing(",
     "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
 }

@@ -752,7 +752,10 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // the three mask blurs (of the mask front in d_mb_) as one horizontal and
   // one vertical launch over nine planes; then S8.  The full B mask only for
   // the stage dumps: Compare itself samples it at (3j + 3, 3i + 3) alone.
-  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc);
+  // (raw blurred mask planes for the stage dumps of the masks and of the
+  // combined value; the search's passes apply the mask LUTs per sample in
+  // the vertical pass and combine without them)
+  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc || dbg->combined);
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -773,7 +776,13 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
                                                                    scale_stride_));
     for (int p = 0; p < 9; ++p) bp.in[p] = bp.out[p];
     for (int p = 0; p < 6; ++p) bp.out[p] = d_bl_ + p * dn;
-    for (int c = 0; c < 3; ++c) bp.out[6 + c] = d_ma_ + c * n;
+    // mask samples: the LUT pairs (masks -> d_ma_, DC masks -> d_mb_, free
+    // after the h pass) -- except for the stage dumps, which want the raw
+    // blurred planes (k_mask_full, k_combine)
+    for (int c = 0; c < 3; ++c) {
+      bp.out[6 + c] = d_ma_ + c * n;
+      bp.out2[6 + c] = full_mask ? nullptr : d_mb_ + c * n;
+    }
     const dim3 gv = BlurVStreamGrid(w_, h_, 9, bp);  // fills bp's packed-grid fields
     GZ_TIMED("blur_v", k_blur_vstream<kBlurLfMask><<<gv, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
     GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
@@ -785,12 +794,18 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     if (!d2h(dbg->mask, d_mb_, 3 * n)) return false;
     if (!d2h(dbg->mask_dc, d_tmp_, 3 * n)) return false;
   }
-  // S14/S15: combine channels (+ mask LUTs, + sqrt)
-  float* dbg_comb = nullptr;
-  if (dbg && dbg->combined) dbg_comb = d_bl_;  // scratch, consumed below
-  GZ_TIMED("combine", k_combine<<<PixGrid(rw_, rh_), 256, 0, s>>>(mk, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_,
-                                               d_resval_, dbg_comb));
-  if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
+  // S14/S15: combine channels (+ sqrt; + the mask LUTs for the stage dumps)
+  if (full_mask) {
+    float* dbg_comb = nullptr;
+    if (dbg->combined) dbg_comb = d_bl_;  // scratch, consumed below
+    GZ_TIMED("combine", k_combine<<<PixGrid(rw_, rh_), 256, 0, s>>>(mk, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_,
+                                                 d_resval_, dbg_comb));
+    if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
+  } else {
+    const MaskPlanes mkdc = MaskPlanesOf(d_mb_, n, true);
+    GZ_TIMED("combine_channels", k_combine_channels<<<PixGrid(rw_, rh_), 256, 0, s>>>(
+        mk, mkdc, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_, d_resval_));
+  }
   // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
   {
     const int wc = w_ - 5, hc = h_ - 5;

@@ -102,6 +102,10 @@ constexpr int kMaxBlurPlanes = 9;  // the merged sigma-14 + mask launches
 struct BlurPlanes {
   const float* in[kMaxBlurPlanes];
   float* out[kMaxBlurPlanes];
+  // mask planes of a vertical pass: when set, out gets MaskOpt's LUT value
+  // MaskX/Y/B (the mask) of each blurred sample and out2 MaskDcX/Y/B (the
+  // DC mask), both times kGlobalScale^-2 (the S13 tail, once per sample)
+  float* out2[kMaxBlurPlanes];
   int sig[kMaxBlurPlanes];
   // packed 1-D grid over the planes' (tile, row) work items: plane p owns
   // workgroups [start[p], start[p+1]), tiles[p] 256-wide tiles per row
@@ -412,6 +416,16 @@ __device__ __forceinline__ void ycbcr_to_linear(int y, int cb, int cr, float out
 // ---------------------------------------------------------------------------
 // Mask LUT stage at one pixel (MaskOpt tail, :1234-1263)
 // ---------------------------------------------------------------------------
+
+// MaskOpt's tail for one channel c of a blurred mask sample s:
+// (MaskX/Y/B, MaskDcX/Y/B) * kGlobalScale^-2 -- mask_luts' operations.
+__device__ __forceinline__ void mask_lut_pair(int c, float sv, float* m, float* mdc) {
+  const float p = (c == 0 ? 232.206464018f : (c == 1 ? 22.9455222245f : 503.962310606f)) * sv;
+  const float gs = static_cast<float>(1.0 / static_cast<double>(14.921561160295326f));
+  const float gs2 = gs * gs;
+  *m = interp_clamp_neg_f(c_tab.mask_lut[c], 512, p) * gs2;
+  *mdc = interp_clamp_neg_f(c_tab.mask_lut[3 + c], 512, p) * gs2;
+}
 
 __device__ __forceinline__ void mask_luts(float s0, float s1, float s2, float mask[3],
                                           float mask_dc[3]) {
