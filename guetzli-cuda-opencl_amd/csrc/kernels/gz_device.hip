@@ -443,7 +443,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jzz_), nc * sizeof(int16_t));
   alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
   alloc(reinterpret_cast<void**>(&e->d_jhist_), 6 * 256 * 4 + 16);
-  alloc(&e->d_jcodes_, sizeof(JpegCodeTables));
+  alloc(&e->d_jcodes_, sizeof(JpegCodesPacked));
   alloc(reinterpret_cast<void**>(&e->d_jbitlen_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_jbitoff_), static_cast<size_t>(e->nb_ + 1) * 4);
   // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
@@ -455,7 +455,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_jhist_), e->h_jhist_, 0) != hipSuccess)
     ok = false;
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodeTables)) != hipSuccess)
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodesPacked)) != hipSuccess)
     ok = false;
   if (ok && (hipMemsetAsync(e->d_jhist_, 0, 6 * 256 * 4 + 16, s) != hipSuccess ||
              hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess))
@@ -1059,9 +1059,13 @@ bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
-  *h_jcodes_ = codes;
-  GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodeTables), hipMemcpyHostToDevice, s));
-  const JpegCodeTables* dc = static_cast<const JpegCodeTables*>(d_jcodes_);
+  for (int c = 0; c < 3; ++c)
+    for (int i = 0; i < 256; ++i) {
+      h_jcodes_->e[c][i] = (static_cast<uint32_t>(codes.dc_len[c][i]) << 16) | codes.dc_code[c][i];
+      h_jcodes_->e[c][256 + i] = (static_cast<uint32_t>(codes.ac_len[c][i]) << 16) | codes.ac_code[c][i];
+    }
+  GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodesPacked), hipMemcpyHostToDevice, s));
+  const JpegCodesPacked* dc = static_cast<const JpegCodesPacked*>(d_jcodes_);
   uint32_t* words = d_jwords_[jslot_];
   const unsigned mcu_groups = static_cast<unsigned>((nb_ + 3) / 4);
   GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_));

@@ -25,6 +25,12 @@ struct CoeffDataHost {  // guetzli::CoeffData (processor.h:29-32)
 // Optional host destinations for stage-level parity tests.
 // Per component Huffman code (length, code) of every symbol, as the device
 // entropy coder consumes them.
+// The same codes as the device reads them: (length << 16) | code per
+// symbol, e[comp][0..255] DC, e[comp][256..511] AC (one load per lookup).
+struct JpegCodesPacked {
+  uint32_t e[3][512];
+};
+
 struct JpegCodeTables {
   uint8_t dc_len[3][256];
   uint8_t ac_len[3][256];
@@ -196,7 +202,7 @@ class Engine {
   int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
   uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
   uint32_t* d_jhist_ = nullptr;    //   6 x 256 counts + chroma non-zeros (u64) + done counter
-  void* d_jcodes_ = nullptr;       //   JpegCodeTables
+  void* d_jcodes_ = nullptr;       //   JpegCodesPacked
   int* d_jbitlen_ = nullptr;       //   [blocks]
   int* d_jbitoff_ = nullptr;       //   [blocks + 1]
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
@@ -206,7 +212,7 @@ class Engine {
   size_t jwords_cap_ = 0;
   uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + (0xff count, total bits),
   uint32_t* m_jhist_ = nullptr;    //   written by the kernels through this mapped address
-  JpegCodeTables* h_jcodes_ = nullptr;
+  JpegCodesPacked* h_jcodes_ = nullptr;
   uint8_t* h_jbytes_ = nullptr;
   size_t h_jbytes_cap_ = 0;
   int* h_zero_off_ = nullptr;      // pinned
