@@ -14,6 +14,7 @@
 
 #include "host/jpeg_encode.h"
 #include "host/jpeg_reader.h"
+#include "host/png_reader.h"
 #include "host/jpeg_writer.h"
 #include "host/processor.h"
 #include "host/strips.h"
@@ -69,6 +70,23 @@ double gz_butteraugli_score_for_quality(double quality) {
 }
 
 void gz_free(void* p) { std::free(p); }
+
+gz_status gz_png_decode(const uint8_t* png, size_t png_len, int* width, int* height,
+                        uint8_t** rgb_out) {
+  if (!png || !width || !height || !rgb_out) return SetError(GZ_ERR_INVALID_ARG, "png_decode: bad argument");
+  std::vector<uint8_t> rgb;
+  std::string err;
+  int w = 0, h = 0;
+  if (!gz::ReadPng(png, png_len, &w, &h, &rgb, &err))
+    return SetError(GZ_ERR_INVALID_ARG, "png_decode: " + err);
+  uint8_t* buf = static_cast<uint8_t*>(std::malloc(rgb.size()));
+  if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "out of host memory");
+  std::memcpy(buf, rgb.data(), rgb.size());
+  *width = w;
+  *height = h;
+  *rgb_out = buf;
+  return GZ_OK;
+}
 
 gz_status gz_comparator_create(int device, int width, int height, const uint8_t* rgb,
                                float target_distance, gz_comparator** out) {

@@ -78,7 +78,7 @@ EXPORTED_SYMBOLS = (
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
     "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode", "gz_comparator_distmap",
-    "gz_comparator_compare_blocks",
+    "gz_comparator_compare_blocks", "gz_png_decode",
 )
 
 _lib = None
@@ -114,6 +114,9 @@ def lib():
     L.gz_process_jpeg.argtypes = [i32, ctypes.POINTER(_Params), vp, ctypes.c_size_t,
                                   ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t),
                                   ctypes.POINTER(_Stats)]
+    L.gz_png_decode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                ctypes.POINTER(vp)]
+    L.gz_png_decode.restype = i32
     L.gz_jpeg_decode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(i32), ctypes.POINTER(i32),
                                  ctypes.POINTER(i32), ctypes.POINTER(vp),
                                  ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(vp)]
@@ -337,6 +340,29 @@ def process_jpeg(jpeg, params=None, device=0, return_stats=False):
                                   st.seconds_total, st.seconds_setup, st.seconds_write,
                                   st.seconds_quantize, st.seconds_backend)
     return data
+
+
+def png_decode(png):
+    """ReadPNG of the reference CLI (guetzli.cc:51-156) on the host:
+    (width, height, rgb uint8 array of 3*w*h)."""
+    data = bytes(png)
+    w, h, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_void_p()
+    _check(lib().gz_png_decode(data, len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)),
+           "png_decode")
+    n = 3 * w.value * h.value
+    rgb = np.frombuffer(_take_bytes(p, ctypes.c_size_t(n)), dtype=np.uint8).copy()
+    return w.value, h.value, rgb
+
+
+def process_file(data, params=None, device=0, return_stats=False):
+    """The reference CLI's input dispatch (guetzli.cc:284-310): a PNG file is
+    decoded (png_decode) and encoded from its RGB, anything else is taken as
+    a JPEG file (process_jpeg)."""
+    data = bytes(data)
+    if data[:8] == b"\x89PNG\r\n\x1a\n":
+        w, h, rgb = png_decode(data)
+        return process(rgb, w, h, params, device, return_stats)
+    return process_jpeg(data, params, device, return_stats)
 
 
 def jpeg_decode(jpeg):

@@ -131,6 +131,14 @@ gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jp
 gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* height,
                          int* ncomp, int16_t** coeffs_out, size_t* ncoeffs, uint8_t** rgb_out);
 
+/* ReadPNG of the reference CLI (guetzli/guetzli.cc:51-156; libpng with
+ * PACKING | EXPAND | STRIP_16, alpha blended on black), host only: every PNG
+ * colour type and bit depth, interlaced or not, tRNS.  *rgb_out: RGB8,
+ * 3*w*h bytes, library-allocated (gz_free).  GZ_ERR_INVALID_ARG for what
+ * ReadPNG rejects (the CLI then fails, guetzli.cc:326-330). */
+gz_status gz_png_decode(const uint8_t* png, size_t png_len, int* width, int* height,
+                        uint8_t** rgb_out);
+
 /* ---- one frame over several GPUs (row strips + halo) ------------------ */
 /* The exchange a multi-rank encode needs: an equal-size all-gather (every
  * rank contributes `bytes` bytes, `recv` receives world*bytes in rank order);
