@@ -59,6 +59,16 @@ def inputs():
                                             exif=b"Exif\x00\x00MM\x00*\x00\x00\x00\x08\x00\x00",
                                             comment=b"guetzli-mi355x fixture"), 95),
     }
+    # gray content in three components (R = G = B): a 4:4:4 YCbCr input the
+    # reference encodes (its chroma planes carry only rounding noise); and a
+    # one-component grayscale file, which the reference's ProcessJpegData
+    # rejects (processor.cc:946-949: only 3-component YCbCr input)
+    gray = np.repeat(bees[:120, :160, 1:2], 3, axis=2)
+    out["graycontent_pil_q85_444"] = (pil_jpeg(np.ascontiguousarray(gray), quality=85,
+                                               subsampling=0), 95)
+    buf = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(bees[:120, :160, 1])).save(buf, "JPEG", quality=85)
+    out["gray1_pil_q85"] = (buf.getvalue(), 95)
     # a guetzli output as input (SOF1, guetzli's own table layout)
     tmp = tempfile.mkdtemp()
     raw = os.path.join(tmp, "bees88.rgb")
@@ -84,7 +94,7 @@ def main():
         r = subprocess.run([REF, "decode", path, rgb_p, co_p], capture_output=True, text=True)
         if r.returncode == 0:
             info = json.loads(r.stdout)
-            e.update(w=info["w"], h=info["h"],
+            e.update(w=info["w"], h=info["h"], ncomp=info["ncomp"],
                      rgb_sha256=hashlib.sha256(open(rgb_p, "rb").read()).hexdigest(),
                      coeffs_sha256=hashlib.sha256(open(co_p, "rb").read()).hexdigest())
         out_p = os.path.join(tmp, "o.jpg")

@@ -34,9 +34,11 @@ def test_read_and_decode_match_reference(name):
     data = _data(name)
     assert _sha(data) == e["input_sha256"]
     w, h, nc, coeffs, rgb = gz.jpeg_decode(data)
-    assert (w, h, nc) == (e["w"], e["h"], 3)
+    assert (w, h, nc) == (e["w"], e["h"], e.get("ncomp", 3))
     assert _sha(coeffs.tobytes()) == e["coeffs_sha256"]
-    assert _sha(rgb.tobytes()) == e["rgb_sha256"]  # 4:2:0 via the fancy upsampler
+    # (4:2:0 via the fancy upsampler; a one-component file decodes to no RGB,
+    # as DecodeJpegToRGB returns an empty vector)
+    assert _sha(b"" if rgb is None else rgb.tobytes()) == e["rgb_sha256"]
 
 
 def test_progressive_input_decodes_ac_coefficients():
@@ -60,7 +62,7 @@ def test_reader_rejects_invalid_input(bad):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", sorted(n for n in CASES if "_420" not in n))
+@pytest.mark.parametrize("name", sorted(n for n in CASES if "_420" not in n and CASES[n]["reference_ok"]))
 def test_process_jpeg_matches_reference(name):
     e = CASES[name]
     assert e["reference_ok"]
@@ -75,6 +77,16 @@ def test_process_jpeg_420_is_unsupported():
     with pytest.raises(gz.GuetzliError) as ei:
         gz.process_jpeg(_data("synth_pil_q85_420"), gz.Params.for_quality(95))
     assert ei.value.status == 4  # GZ_ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_process_jpeg_one_component_rejected_as_reference():
+    """A one-component (grayscale) JPEG: the reference's Process returns
+    false (ProcessJpegData accepts only 3-component YCbCr input), and so does
+    this build -- with an error, not an encode."""
+    assert not CASES["gray1_pil_q85"]["reference_ok"]
+    with pytest.raises(gz.GuetzliError):
+        gz.process_jpeg(_data("gray1_pil_q85"), gz.Params.for_quality(95))
 
 
 @pytest.mark.gpu
