@@ -9,6 +9,8 @@
 // coefficient arrays over the MCU-padded block grid (:140-152).
 #include "host/jpeg_reader.h"
 
+#include "host/image420.h"
+
 #include <string.h>
 
 #include <algorithm>
@@ -471,35 +473,8 @@ struct Reader {
   }
 };
 
-// libjpeg-exact integer IDCT coefficients (guetzli/idct.cc:29-38)
-const int kIdctM[64] = {
-    8192, 11363, 10703, 9633,   8192,  6437,   4433,   2260,   8192, 9633,  4433,  -2259, -8192,
-    -11362, -10704, -6436, 8192, 6437, -4433,  -11362, -8192, 2261,   10704,  9633, 8192,  2260,
-    -10703, -6436, 8192, 9633,  -4433, -11363, 8192,   -2260, -10703, 6436,   8192, -9633, -4433,
-    11363,  8192,  -6437, -4433, 11362, -8192, -2261,  10704, -9633,  8192,   -9633, 4433, 2259,
-    -8192,  11362, -10704, 6436, 8192,  -11363, 10703, -9633, 8192,   -6437,  4433,  -2260,
-};
-
 inline int Clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 inline int Fix16(double x) { return static_cast<int>(x * 65536.0 + 0.5); }
-
-// ComputeBlockIDCT (idct.cc:139-161): column pass rounded to int16 at scale
-// 2^11, row pass with the +128 level shift folded into the rounding term.
-void BlockIdct(const coeff_t* in, uint8_t out[64]) {
-  int16_t col[64];
-  for (int iy = 0; iy < 8; ++iy)
-    for (int ix = 0; ix < 8; ++ix) {
-      unsigned acc = 0;
-      for (int u = 0; u < 8; ++u) acc += static_cast<unsigned>(kIdctM[8 * iy + u] * in[8 * u + ix]);
-      col[8 * iy + ix] = static_cast<int16_t>((static_cast<int>(acc) + (1 << 10)) >> 11);
-    }
-  for (int iy = 0; iy < 8; ++iy)
-    for (int ix = 0; ix < 8; ++ix) {
-      unsigned acc = 0;
-      for (int u = 0; u < 8; ++u) acc += static_cast<unsigned>(kIdctM[8 * ix + u] * col[8 * iy + u]);
-      out[8 * iy + ix] = static_cast<uint8_t>(Clamp255((static_cast<int>(acc) + (257 << 17)) >> 18));
-    }
-}
 
 }  // namespace
 
@@ -547,83 +522,16 @@ bool CheckJpegSanity(const JpegData& jpg) {
   return true;
 }
 
-namespace {
-
-// One component of guetzli::OutputImage (output_image.cc:36-50): 16-bit
-// pixels at full image resolution (value << 4), blocks at 1 / factor.
-struct DecodePlane {
-  int w, h, fx, fy, wib, hib;
-  std::vector<uint16_t> px;
-
-  // UpdatePixelsForBlock (output_image.cc:135-205).  Factor 2: the 10x10
-  // subsampled neighbourhood of the block (its 8x8 IDCT bytes, a ring
-  // rebuilt from the already-upsampled pixels by inverting the fancy
-  // upsampler, edge replication outside the image; filled rows 1..9 then
-  // row 0, columns 1..9 then column 0), then the 3x3 fancy upsampler over
-  // the block's 16x16 area plus one pixel above / left.
-  void Update(int bx, int by, const uint8_t idct[64]) {
-    if (fx == 1 && fy == 1) {
-      for (int iy = 0; iy < 8 && 8 * by + iy < h; ++iy)
-        for (int ix = 0; ix < 8 && 8 * bx + ix < w; ++ix)
-          px[(8 * by + iy) * w + 8 * bx + ix] = static_cast<uint16_t>(idct[8 * iy + ix] << 4);
-      return;
-    }
-    constexpr int E = 10;
-    uint16_t sub[E * E];
-    for (int j = 0; j < E; ++j) {
-      const int row = j < 9 ? j + 1 : 0;
-      const int y0 = by * 16 + (j < 9 ? 2 * j : -2);
-      for (int i = 0; i < E; ++i) {
-        const int col = i < 9 ? i + 1 : 0;
-        const int x0 = bx * 16 + (i < 9 ? 2 * i : -2);
-        uint16_t* d = &sub[row * E + col];
-        if (x0 < 0) {
-          *d = d[1];
-        } else if (y0 < 0) {
-          *d = d[E];
-        } else if (x0 >= w) {
-          *d = d[-1];
-        } else if (y0 >= h) {
-          *d = d[-E];
-        } else if (i < 8 && j < 8) {
-          *d = static_cast<uint16_t>(idct[8 * j + i] << 4);
-        } else {
-          const int y1 = y0 > 0 ? y0 - 1 : 0, x1 = x0 > 0 ? x0 - 1 : 0;
-          *d = static_cast<uint16_t>((px[y0 * w + x0] * 9 + px[y1 * w + x1] - 3 * px[y0 * w + x1] -
-                                      3 * px[y1 * w + x0]) >> 2);
-        }
-      }
-    }
-    const int xa = std::max(bx * 16 - 1, 0), xb = std::min(bx * 16 + 16, w - 1);
-    const int ya = std::max(by * 16 - 1, 0), yb = std::min(by * 16 + 16, h - 1);
-    for (int y = ya; y <= yb; ++y) {
-      const int r0 = ((y & ~1) / 2 - by * 8 + 1) * E, dr = (y & 1) ? E : -E;
-      for (int x = xa; x <= xb; ++x) {
-        const int k = r0 + (x & ~1) / 2 - bx * 8 + 1, dc = (x & 1) ? 1 : -1;
-        px[y * w + x] = static_cast<uint16_t>(
-            (sub[k] * 9 + sub[k + dr] * 3 + sub[k + dc] * 3 + sub[k + dc + dr]) >> 4);
-      }
-    }
-  }
-};
-
-}  // namespace
-
 bool DecodeJpegToRGB(const JpegData& jpg, std::vector<uint8_t>* rgb) {
   if (!(JpegIs444(jpg) || JpegIs420(jpg)) || !HasYCbCrColorSpace(jpg)) return false;
   const int w = jpg.width, h = jpg.height;
-  DecodePlane plane[3];
+  SubsampledPlane plane[3];
   for (int c = 0; c < 3; ++c) {
     const JpegComponent& comp = jpg.components[c];
     const int* q = jpg.quant[comp.quant_idx].values;
-    DecodePlane& P = plane[c];
-    P.w = w;
-    P.h = h;
-    P.fx = jpg.max_h_samp_factor / comp.h_samp_factor;
-    P.fy = jpg.max_v_samp_factor / comp.v_samp_factor;
-    P.wib = (w + 8 * P.fx - 1) / (8 * P.fx);
-    P.hib = (h + 8 * P.fy - 1) / (8 * P.fy);
-    P.px.assign(static_cast<size_t>(w) * h, 128 << 4);
+    SubsampledPlane& P = plane[c];
+    // (4:4:4 or 4:2:0: both directions share the factor)
+    P.Reset(w, h, jpg.max_h_samp_factor / comp.h_samp_factor);
     // CopyFromJpegData: blocks in raster order (the factor-2 update reads the
     // pixels of blocks already set), coeff * quant stored as coeff_t
     for (int by = 0; by < P.hib; ++by)
@@ -632,7 +540,7 @@ bool DecodeJpegToRGB(const JpegData& jpg, std::vector<uint8_t>* rgb) {
         coeff_t deq[64];
         for (int k = 0; k < 64; ++k) deq[k] = static_cast<coeff_t>(src[k] * q[k]);
         uint8_t idct[64];
-        BlockIdct(deq, idct);
+        BlockIdctBytes(deq, idct);
         P.Update(bx, by, idct);
       }
   }
@@ -652,7 +560,7 @@ bool DecodeJpegToRGB(const JpegData& jpg, std::vector<uint8_t>* rgb) {
     for (int x = 0; x < w; ++x) {
       const size_t p = static_cast<size_t>(y) * w + x;
       int v[3];
-      for (int c = 0; c < 3; ++c) v[c] = (plane[c].px[p] + 8 - (x & 1)) >> 4;
+      for (int c = 0; c < 3; ++c) v[c] = PixelByte(plane[c].px[p], x);
       (*rgb)[3 * p] = static_cast<uint8_t>(Clamp255(v[0] + cr_r[v[2]]));
       (*rgb)[3 * p + 1] = static_cast<uint8_t>(Clamp255(v[0] + ((cr_g[v[2]] + cb_g[v[1]]) >> 16)));
       (*rgb)[3 * p + 2] = static_cast<uint8_t>(Clamp255(v[0] + cb_b[v[1]]));
