@@ -366,6 +366,9 @@ static gz::ProcessParams ToProcessParams(const gz_params* params) {
   gz::ProcessParams pp;
   pp.butteraugli_target = params->butteraugli_target;
   pp.clear_metadata = params->clear_metadata != 0;
+  pp.try_420 = params->try_420 != 0;
+  pp.force_420 = params->force_420 != 0;
+  pp.use_silver_screen = params->use_silver_screen != 0;
   pp.zeroing_greedy_lookahead = params->zeroing_greedy_lookahead;
   pp.new_zeroing_model = params->new_zeroing_model != 0;
   return pp;
@@ -377,8 +380,9 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
                              const gz_collectives* coll = nullptr) {
   if (!params || !rgb || !jpeg_out || !jpeg_size || w <= 0 || h <= 0)
     return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
-  if (params->try_420 || params->force_420)
-    return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output is not supported");
+  // (the strip decomposition of one frame runs the 4:4:4 search only)
+  if (coll && (params->try_420 || params->force_420))
+    return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output of a strip-decomposed frame is not supported");
   const gz::ProcessParams pp = ToProcessParams(params);
   gz::ProcessResult res;
   std::string err;
@@ -442,8 +446,6 @@ gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jp
                           uint8_t** jpeg_out, size_t* jpeg_size, gz_process_stats* stats) {
   if (!params || !jpeg || !jpeg_out || !jpeg_size)
     return SetError(GZ_ERR_INVALID_ARG, "process_jpeg: bad argument");
-  if (params->try_420 || params->force_420)
-    return SetError(GZ_ERR_UNSUPPORTED, "process_jpeg: 4:2:0 output is not supported");
   gz::ProcessResult res;
   std::string err;
   const int rc = gz::ProcessJpeg(device, ToProcessParams(params), jpeg, jpeg_len, &res, &err);

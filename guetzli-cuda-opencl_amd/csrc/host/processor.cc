@@ -436,6 +436,68 @@ bool HipButteraugliComparator::BlockZeroingCandidates(const CoeffImage& img, con
   return true;
 }
 
+bool HipButteraugliComparator::SetOriginalCoeffs420(const JpegData& jpg420) {
+  // the luma at the engine's block width (the 4:2:0 file pads Y to whole
+  // MCUs), the chroma as stored; q = 1, so these are the raw values the
+  // zeroing keys and the back end read (processor.cc:653-657, 865-868)
+  const int bw = engine_->block_w(), bh = engine_->block_h();
+  const int cbw = (w_ + 15) / 16, cbh = (h_ + 15) / 16;
+  if (jpg420.components.size() != 3) {
+    err_ = "4:2:0 originals need 3 components";
+    return false;
+  }
+  std::vector<coeff_t> y(static_cast<size_t>(bw) * bh * 64), c[2];
+  const JpegComponent& jy = jpg420.components[0];
+  for (int by = 0; by < bh; ++by)
+    std::memcpy(&y[static_cast<size_t>(by) * bw * 64], &jy.coeffs[static_cast<size_t>(by) * jy.width_in_blocks * 64],
+                static_cast<size_t>(bw) * 64 * sizeof(coeff_t));
+  for (int k = 0; k < 2; ++k) {
+    const JpegComponent& jc = jpg420.components[1 + k];
+    c[k].resize(static_cast<size_t>(cbw) * cbh * 64);
+    for (int by = 0; by < cbh; ++by)
+      std::memcpy(&c[k][static_cast<size_t>(by) * cbw * 64], &jc.coeffs[static_cast<size_t>(by) * jc.width_in_blocks * 64],
+                  static_cast<size_t>(cbw) * 64 * sizeof(coeff_t));
+  }
+  orig_on_device_ = false;  // (the 4:4:4 originals are gone from the device)
+  device_ = CoeffCursor();
+  if (!engine_->SetOriginal420(y.data(), c[0].data(), c[1].data())) {
+    err_ = engine_->error();
+    return false;
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::Compare420(const Image420& img) {
+  const auto t0 = Clock::now();
+  device_ = CoeffCursor();
+  if (!engine_->Set420(img.y.data(), img.c[0].data(), img.c[1].data(), img.plane[0].px.data(),
+                       img.plane[1].px.data()) ||
+      !engine_->Compare(&distance_, block_max_.data(), nullptr)) {
+    err_ = engine_->error();
+    return false;
+  }
+  ++compares;
+  seconds_compare += Since(t0);
+  return true;
+}
+
+bool HipButteraugliComparator::BlockZeroingCandidates420(Image420* img, int comp_mask, int lookahead,
+                                                         bool new_model, std::vector<int>* offsets,
+                                                         std::vector<uint8_t>* idx,
+                                                         std::vector<float>* err) {
+  const auto t0 = Clock::now();
+  device_ = CoeffCursor();
+  if (!engine_->Set420(img->y.data(), img->c[0].data(), img->c[1].data(), img->plane[0].px.data(),
+                       img->plane[1].px.data()) ||
+      !engine_->BlockZeroingCandidates420(comp_mask, target_, lookahead, new_model, offsets, idx, err,
+                                          img->plane[0].px.data(), img->plane[1].px.data())) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_zeroing += Since(t0);
+  return true;
+}
+
 double HipButteraugliComparator::ScoreOutputSize(int size) const {
   return ScoreJPEG(distance_, size, target_);
 }
@@ -554,7 +616,7 @@ bool CompareQuantData(const QuantData& a, const QuantData& b) {
 // Binary search over the heuristic quantization "score" (processor.cc:206-308).
 class QuantMatrixGenerator {
  public:
-  QuantMatrixGenerator() {
+  explicit QuantMatrixGenerator(bool downsample = false) : downsample_(downsample) {
     for (int k = 0; k < kDCTBlockSize; ++k) total_csf_ += 3.0 * ContrastSensitivity(k);
   }
   bool GetNext(int q[3][kDCTBlockSize]) {
@@ -562,7 +624,7 @@ class QuantMatrixGenerator {
       double hscore;
       if (hscore_b_ == -1.0) {
         if (hscore_a_ == -1.0) {
-          hscore = total_csf_;
+          hscore = downsample_ ? 0.0 : total_csf_;
         } else if (hscore_a_ < 5.0 * total_csf_) {
           hscore = hscore_a_ + total_csf_;
         } else {
@@ -610,6 +672,7 @@ class QuantMatrixGenerator {
       score -= 3.0 * ContrastSensitivity(kJPEGNaturalOrder[k]);
     }
   }
+  bool downsample_;
   double hscore_a_ = -1.0, hscore_b_ = -1.0, total_csf_ = 0.0;
   std::vector<QuantData> quants_;
 };
@@ -851,6 +914,13 @@ class Processor {
                               double target_mul, bool stop_early,
                               const std::vector<int>& offsets, const std::vector<uint8_t>& coeffs,
                               const std::vector<float>& errors, std::string* err);
+  // The 4:2:0 pass (processor.cc:989-1016, downsample = 1) on the host model
+  // Image420, entropy coded on the host.
+  int Run420(const JpegData& jpg_in, std::string* err);
+  bool TryQuantMatrix420(const JpegData& jpg, float target_mul, const int q[3][kDCTBlockSize],
+                         Image420* img, QuantData* data, std::string* err);
+  bool SelectFrequencyMasking420(const JpegData& jpg, Image420* img, int comp_mask,
+                                 double target_mul, bool stop_early, std::string* err);
 
   ProcessParams params_;
   Comparator* cmp_;
@@ -1216,11 +1286,63 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   return true;
 }
 
+// RemoveOriginalQuantization, processor.cc:94-107: coefficients times their
+// quantization, quant tables of ones; q_in receives the originals.
+void RemoveOriginalQuantization(JpegData* jpg, int q_in[3][kDCTBlockSize]) {
+  for (int i = 0; i < 3; ++i) {
+    JpegComponent& c = jpg->components[i];
+    const int* q = jpg->quant[c.quant_idx].values;
+    std::memcpy(q_in[i], q, sizeof(q_in[i]));
+    for (size_t j = 0; j < c.coeffs.size(); ++j) c.coeffs[j] = static_cast<coeff_t>(c.coeffs[j] * q[j % 64]);
+  }
+  int ones[3][kDCTBlockSize];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < kDCTBlockSize; ++j) ones[i][j] = 1;
+  SaveQuantTables(ones, jpg);
+}
+
+// IsGrayscale, processor.cc:921-929
+bool IsGrayscale(const JpegData& jpg) {
+  for (int c = 1; c < 3; ++c)
+    for (coeff_t v : jpg.components[c].coeffs)
+      if (v != 0) return false;
+  return true;
+}
+
+// UpdateACHistogram, processor.cc:491-515
+void UpdateACHistogram(int weight, const coeff_t* coeffs, const int* q, JpegHistogram* h) {
+  int r = 0;
+  for (int k = 1; k < 64; ++k) {
+    const int k_nat = kJPEGNaturalOrder[k];
+    const coeff_t coeff = coeffs[k_nat];
+    if (coeff == 0) {
+      ++r;
+      continue;
+    }
+    while (r > 15) {
+      h->Add(0xf0, weight);
+      r -= 16;
+    }
+    h->Add((r << 4) + Log2FloorNonZero(std::abs(coeff / q[k_nat])) + 1, weight);
+    r = 0;
+  }
+  if (r > 0) h->Add(0, weight);
+}
+
 int Processor::Run(const JpegData& jpg_in, std::string* err) {
-  // ProcessJpegData, processor.cc:931-1020 (4:4:4, no 4:2:0 trial)
+  // ProcessJpegData, processor.cc:931-1020
   if (params_.butteraugli_target > 2.0f) {
     if (err) *err = "butteraugli target above 2.0 (quality below 84) is not supported";
     return GZ_ERR_INVALID_ARG;
+  }
+  if (jpg_in.components.size() != 3 || !HasYCbCrColorSpace(jpg_in)) {
+    if (err) *err = "Only YUV color space input jpeg is supported";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  const bool input_is_420 = JpegIs420(jpg_in);
+  if (!input_is_420 && !JpegIs444(jpg_in)) {
+    if (err) *err = "Unsupported sampling factors";
+    return GZ_ERR_UNSUPPORTED;
   }
   std::string encoded;
   OutputJpeg(jpg_in, &encoded);
@@ -1229,44 +1351,303 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
     res_->jpeg = encoded;
     return GZ_OK;
   }
-  auto remove_quant = [](JpegData* jpg, int q_in[3][kDCTBlockSize]) {
-    // RemoveOriginalQuantization, processor.cc:94-107
-    for (int i = 0; i < 3; ++i) {
-      JpegComponent& c = jpg->components[i];
-      const int* q = jpg->quant[c.quant_idx].values;
-      std::memcpy(q_in[i], q, sizeof(q_in[i]));
-      for (size_t j = 0; j < c.coeffs.size(); ++j) c.coeffs[j] = static_cast<coeff_t>(c.coeffs[j] * q[j % 64]);
-    }
-    int ones[3][kDCTBlockSize];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < kDCTBlockSize; ++j) ones[i][j] = 1;
-    SaveQuantTables(ones, jpg);
-  };
   int q_in[3][kDCTBlockSize];
   JpegData jpg = jpg_in;
-  remove_quant(&jpg, q_in);
+  RemoveOriginalQuantization(&jpg, q_in);
   auto device_error = [&]() {
     Fail(err);
     return GZ_ERR_DEVICE;
   };
-  if (!cmp_->SetOriginalCoeffs(jpg)) return device_error();
   CoeffImage img;
-  img.Init(jpg.width, jpg.height);
-  img.CopyFromJpegData(jpg);
-  if (!cmp_->Compare(img)) return device_error();
+  if (!input_is_420) {
+    if (!cmp_->SetOriginalCoeffs(jpg)) return device_error();
+    img.Init(jpg.width, jpg.height);
+    img.CopyFromJpegData(jpg);
+    if (!cmp_->Compare(img)) return device_error();
+  } else {
+    Image420 im;
+    im.Init(jpg.width, jpg.height);
+    im.CopyFromJpegData(jpg);
+    if (!cmp_->Compare420(im)) return device_error();
+  }
   MaybeOutput(encoded);
-  img.CopyFromJpegData(jpg);
-  int best_q[3][kDCTBlockSize];
-  std::memcpy(best_q, q_in, sizeof(best_q));
-  bool ok = false;
-  if (!SelectQuantMatrix(jpg, best_q, &img, &ok, err)) return GZ_ERR_DEVICE;
-  if (!ok)
-    for (int c = 0; c < 3; ++c)
-      for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
-  if (!cmp_->QuantizeFromOriginal(best_q, &img)) return device_error();
-  if (!SelectFrequencyMasking(jpg, &img, 7, 1.0, false, err)) return GZ_ERR_DEVICE;
+  const int try_420 = (input_is_420 || params_.force_420 || (params_.try_420 && !IsGrayscale(jpg_in))) ? 1 : 0;
+  const int force_420 = (input_is_420 || params_.force_420) ? 1 : 0;
+  for (int downsample = force_420; downsample <= try_420; ++downsample) {
+    if (downsample) {
+      const int rc = Run420(jpg_in, err);
+      if (rc != GZ_OK) return rc;
+      continue;
+    }
+    img.CopyFromJpegData(jpg);
+    int best_q[3][kDCTBlockSize];
+    std::memcpy(best_q, q_in, sizeof(best_q));
+    bool ok = false;
+    if (!SelectQuantMatrix(jpg, best_q, &img, &ok, err)) return GZ_ERR_DEVICE;
+    if (!ok)
+      for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
+    if (!cmp_->QuantizeFromOriginal(best_q, &img)) return device_error();
+    if (!SelectFrequencyMasking(jpg, &img, 7, 1.0, false, err)) return GZ_ERR_DEVICE;
+  }
+  FlushOutput();
   if (kept_on_device_ && !cmp_->DeviceFetchKept(&res_->jpeg)) return device_error();
   return GZ_OK;
+}
+
+int Processor::Run420(const JpegData& jpg_in, std::string* err) {
+  // processor.cc:990-1016 with downsample = 1
+  FlushOutput();
+  int q_in[3][kDCTBlockSize];
+  JpegData jpg = jpg_in;
+  RemoveOriginalQuantization(&jpg, q_in);
+  JpegData jpg420;
+  if (JpegIs420(jpg)) {
+    // already subsampled (DownsampleImage leaves it): OutputImage of it,
+    // saved back (whole MCUs, padding blocks re-derived)
+    Image420 t;
+    t.Init(jpg.width, jpg.height);
+    t.CopyFromJpegData(jpg);
+    jpg420.app_data = jpg.app_data;
+    jpg420.com_data = jpg.com_data;
+    t.SaveToJpegData(&jpg420);
+  } else if (!DownsampleToJpegData420(jpg, params_.use_silver_screen, &jpg420)) {
+    // (all-zero chroma: the reference keeps 4:4:4 and continues with one
+    // grayscale component)
+    if (err) *err = "4:2:0 pass of an image without chroma is not supported";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  if (jpg420.components.size() != 3) {
+    if (err) *err = "4:2:0 pass of an image without chroma is not supported";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  auto device_error = [&]() {
+    Fail(err);
+    return GZ_ERR_DEVICE;
+  };
+  if (!cmp_->SetOriginalCoeffs420(jpg420)) return device_error();
+  Image420 img;
+  img.Init(jpg420.width, jpg420.height);
+  // SelectQuantMatrix (processor.cc:340-372) with the downsampling generator
+  int best_q[3][kDCTBlockSize];
+  std::memcpy(best_q, q_in, sizeof(best_q));
+  {
+    QuantMatrixGenerator qgen(true);
+    const float target_mul_high = 0.97f, target_mul_low = 0.95f;
+    QuantData best;
+    if (!TryQuantMatrix420(jpg420, target_mul_high, best_q, &img, &best, err)) return GZ_ERR_DEVICE;
+    for (;;) {
+      int q_next[3][kDCTBlockSize];
+      if (!qgen.GetNext(q_next)) break;
+      QuantData data;
+      if (!TryQuantMatrix420(jpg420, target_mul_high, q_next, &img, &data, err)) return GZ_ERR_DEVICE;
+      qgen.Add(data);
+      if (CompareQuantData(data, best)) {
+        best = data;
+        if (data.dist_ok && !cmp_->DistanceOK(target_mul_low)) break;
+      }
+    }
+    std::memcpy(best_q, best.q, sizeof(best.q));
+    if (!best.dist_ok)
+      for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
+  }
+  const auto tq = Clock::now();
+  img.CopyFromJpegData(jpg420);
+  img.ApplyGlobalQuantization(best_q);
+  res_->seconds_quantize += Since(tq);
+  if (!SelectFrequencyMasking420(jpg420, &img, 1, 0.97f, false, err)) return GZ_ERR_DEVICE;
+  if (!SelectFrequencyMasking420(jpg420, &img, 6, 1.0, true, err)) return GZ_ERR_DEVICE;
+  return GZ_OK;
+}
+
+bool Processor::TryQuantMatrix420(const JpegData& jpg, float target_mul, const int q[3][kDCTBlockSize],
+                                  Image420* img, QuantData* data, std::string* err) {
+  // processor.cc:310-338
+  std::memcpy(data->q, q, sizeof(data->q));
+  const auto tq = Clock::now();
+  img->CopyFromJpegData(jpg);
+  img->ApplyGlobalQuantization(q);
+  res_->seconds_quantize += Since(tq);
+  std::string encoded;
+  {
+    JpegData out;
+    out.app_data = jpg.app_data;
+    out.com_data = jpg.com_data;
+    img->SaveToJpegData(&out);
+    OutputJpeg(out, &encoded);
+  }
+  ++res_->iterations;
+  if (!cmp_->Compare420(*img)) return Fail(err);
+  data->dist_ok = cmp_->DistanceOK(target_mul);
+  data->jpg_size = encoded.size();
+  MaybeOutput(encoded);
+  return true;
+}
+
+bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, int comp_mask,
+                                          double target_mul, bool stop_early, std::string* err) {
+  // processor.cc:559-721 and the back end :723-919 for one pass of the 4:2:0
+  // image (comp_mask 1: Y at factor 1; 6: Cb + Cr at factor 2), serial as
+  // in the reference
+  const int ncomp = static_cast<int>(jpg.components.size());
+  const int last_c = Log2FloorNonZero(static_cast<uint32_t>(comp_mask));
+  if (last_c >= ncomp) return true;
+  const int factor = last_c == 0 ? 1 : 2;
+  const int w = img->w, h = img->h;
+  const int block_width = (w + 8 * factor - 1) / (8 * factor);
+  const int block_height = (h + 8 * factor - 1) / (8 * factor);
+  const int num_blocks = block_width * block_height;
+  if (!cmp_->StartBlockComparisons()) return Fail(err);
+  std::vector<int> offsets;
+  std::vector<uint8_t> cand;
+  std::vector<float> cand_err;
+  if (!cmp_->BlockZeroingCandidates420(img, comp_mask, params_.zeroing_greedy_lookahead,
+                                       params_.new_zeroing_model, &offsets, &cand, &cand_err))
+    return Fail(err);
+  cmp_->FinishBlockComparisons();
+  res_->detail["candidates"] += static_cast<double>(cand.size());
+  const auto tb0 = Clock::now();
+  std::vector<JpegHistogram> ac_histograms(ncomp);
+  int jpg_header_size, dc_size;
+  {
+    JpegData out;
+    out.app_data = jpg.app_data;
+    out.com_data = jpg.com_data;
+    img->SaveToJpegData(&out);
+    jpg_header_size = static_cast<int>(JpegHeaderSize(out, params_.clear_metadata));
+    std::vector<JpegHistogram> dc(out.components.size());
+    BuildDCHistograms(out, dc.data());
+    size_t num = dc.size();
+    std::vector<int> idx(num);
+    std::vector<uint8_t> depths(num * JpegHistogram::kSize);
+    dc_size = static_cast<int>(ClusterHistograms(dc.data(), &num, idx.data(), depths.data()));
+    ac_histograms.resize(out.components.size());
+    BuildACHistograms(out, ac_histograms.data());
+  }
+  std::vector<uint8_t> ac_depths;
+  int ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+  const int base_size = jpg_header_size + dc_size + ac_histogram_size +
+                        static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+  int prev_size = base_size;
+  std::vector<float> max_block_error(num_blocks, 0.0f);
+  std::vector<int> last_indexes(num_blocks, 0);
+  res_->seconds_backend += Since(tb0);
+  bool first_up_iter = true;
+  const int cand_n = static_cast<int>(cand_err.size());
+  for (int direction : {1, -1}) {
+    for (;;) {
+      if (stop_early && direction == -1) {
+        FlushOutput();
+        if (prev_size > 1.01 * best_size_) break;
+      }
+      const auto tb = Clock::now();
+      std::vector<std::pair<int, float>> global_order;
+      int blocks_to_change = 0;
+      std::vector<float> block_weight;
+      for (int rblock = 1; rblock <= 4; ++rblock) {
+        block_weight.assign(num_blocks, 0.0f);
+        // the distance map's maximum per searched block (all zero on the first
+        // up iteration, processor.cc:777-780)
+        std::vector<float> bmax(num_blocks, 0.0f);
+        if (!first_up_iter) {
+          const std::vector<float>& m8 = cmp_->block_max_distance();
+          const int bw8 = (w + 7) / 8, bh8 = (h + 7) / 8;
+          for (int by = 0; by < bh8; ++by)
+            for (int bx = 0; bx < bw8; ++bx) {
+              float& d = bmax[(by / factor) * block_width + bx / factor];
+              d = std::max(d, m8[by * bw8 + bx]);
+            }
+        }
+        cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, factor, factor, bmax,
+                                                 &block_weight);
+        global_order.clear();
+        blocks_to_change = 0;
+        for (int bix = 0; bix < num_blocks; ++bix) {
+          const int last_index = last_indexes[bix];
+          const int offset = std::max(0, std::min(offsets[bix], cand_n - 1));
+          const int num_candidates = offsets[bix + 1] - offset;
+          const float* errs = cand_err.data() + offset;
+          const float max_err = max_block_error[bix];
+          if (block_weight[bix] == 0) continue;
+          if (direction > 0) {
+            for (int i = last_index; i < num_candidates; ++i)
+              global_order.push_back(std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]));
+            blocks_to_change += last_index < num_candidates ? 1 : 0;
+          } else {
+            for (int i = last_index - 1; i >= 0; --i)
+              global_order.push_back(std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]));
+            blocks_to_change += last_index > 0 ? 1 : 0;
+          }
+        }
+        if (!global_order.empty()) break;
+      }
+      if (global_order.empty()) {
+        res_->seconds_backend += Since(tb);
+        break;
+      }
+      std::sort(global_order.begin(), global_order.end(),
+                [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; });
+      double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
+      if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
+      const double min_size_delta = base_size * rel_size_delta;
+      const float per_block = direction > 0 ? 2.0f : factor * factor * 0.2f;
+      int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
+      if (first_up_iter) {
+        const float limit = 0.75f * cmp_->BlockErrorLimit();
+        const auto it = std::partition_point(global_order.begin(), global_order.end(),
+                                             [=](const std::pair<int, float>& a) { return a.second < limit; });
+        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, static_cast<int>(it - global_order.begin()));
+        first_up_iter = false;
+      }
+      float val_threshold = 0.0f;
+      int changed_coeffs = 0;
+      int est_jpg_size = prev_size;
+      for (size_t i = 0; i < global_order.size(); ++i) {
+        const int bix = global_order[i].first;
+        const int bx = bix % block_width, by = bix / block_width;
+        const int last_idx = last_indexes[bix];
+        const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+        const int idx = cand[offset + last_idx + std::min(direction, 0)];
+        const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+        const int* quant = img->quant[c];
+        const JpegComponent& comp = jpg.components[c];
+        const int jpg_bix = by * comp.width_in_blocks + bx;
+        const int newval =
+            direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
+        coeff_t block[kDCTBlockSize];
+        std::memcpy(block, img->block(c, bix), sizeof(block));
+        UpdateACHistogram(-1, block, quant, &ac_histograms[c]);
+        block[k] = static_cast<coeff_t>(newval);
+        UpdateACHistogram(1, block, quant, &ac_histograms[c]);
+        img->SetCoeffBlock(c, bix, block);
+        last_indexes[bix] += direction;
+        val_threshold = global_order[i].second;
+        ++changed_coeffs;
+        if (i % 10 == 0) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+        est_jpg_size = jpg_header_size + dc_size + ac_histogram_size +
+                       static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
+        if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta) break;
+      }
+      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
+      ++res_->iterations;
+      if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
+      res_->detail["backend420_changes"] += changed_coeffs;
+      res_->seconds_backend += Since(tb);
+      std::string encoded;
+      {
+        JpegData out;
+        out.app_data = jpg.app_data;
+        out.com_data = jpg.com_data;
+        img->SaveToJpegData(&out);
+        OutputJpeg(out, &encoded);
+      }
+      if (!cmp_->Compare420(*img)) return Fail(err);
+      MaybeOutput(encoded);
+      prev_size = est_jpg_size;
+    }
+  }
+  return true;
 }
 
 }  // namespace
@@ -1348,16 +1729,16 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     return GZ_ERR_INVALID_ARG;
   }
   // ProcessJpegData's input checks (processor.cc:946-963), ahead of the
-  // decode: this build has the 4:4:4 search only
+  // decode
   if (jpg.components.size() != 3 || !HasYCbCrColorSpace(jpg)) {
     if (err) *err = "Only YUV color space input jpeg is supported";
     return GZ_ERR_UNSUPPORTED;
   }
-  if (!JpegIs444(jpg)) {
-    if (err) *err = JpegIs420(jpg) ? "4:2:0 input (the downsampling search) is not supported"
-                                   : "Unsupported sampling factors";
+  if (!JpegIs444(jpg) && !JpegIs420(jpg)) {
+    if (err) *err = "Unsupported sampling factors";
     return GZ_ERR_UNSUPPORTED;
   }
+
   std::vector<uint8_t> rgb;
   if (!DecodeJpegToRGB(jpg, &rgb)) {
     if (err) *err = "input JPEG could not be decoded";

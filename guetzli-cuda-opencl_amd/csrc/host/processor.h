@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "host/image420.h"
 #include "host/jpeg_model.h"
 #include "host/jpeg_writer.h"
 #include "runtime/engine.h"
@@ -94,6 +95,22 @@ class Comparator {
   // QuantizeFromOriginal / BlockZeroingOrders.
   virtual bool SetOriginalCoeffs(const JpegData& jpg) = 0;
   virtual const std::string& error() const = 0;
+
+  // ---- the 4:2:0 pass (processor.cc:989-1016 with downsample = 1) ----
+  // The downsampled image's own q=1 coefficients as the originals
+  // (SaveToJpegData's 4:2:0 layout).
+  virtual bool SetOriginalCoeffs420(const JpegData& jpg420) { return false; }
+  // Compare of the 4:2:0 image: Y from its coefficients, Cb / Cr from the
+  // factor-2 pixel planes as they are.
+  virtual bool Compare420(const Image420& img) { return false; }
+  // The zeroing search of comp_mask 1 (Y) or 6 (Cb + Cr at factor 2) on img;
+  // for 6 the search's SetCoeffBlock calls leave img's chroma pixel state
+  // where the reference's leave it (the kept entries as BlockZeroingCandidates).
+  virtual bool BlockZeroingCandidates420(Image420* img, int comp_mask, int lookahead,
+                                         bool new_model, std::vector<int>* offsets,
+                                         std::vector<uint8_t>* idx, std::vector<float>* err) {
+    return false;
+  }
 };
 
 // ComputeBlockErrorAdjustmentWeights of butteraugli_comparator.cc:169-233
@@ -157,6 +174,11 @@ class HipButteraugliComparator : public Comparator {
                                           std::vector<float>* block_weight) override;
   const std::string& error() const override { return err_; }
   bool SetOriginalCoeffs(const JpegData& jpg) override;
+  bool SetOriginalCoeffs420(const JpegData& jpg420) override;
+  bool Compare420(const Image420& img) override;
+  bool BlockZeroingCandidates420(Image420* img, int comp_mask, int lookahead, bool new_model,
+                                 std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                                 std::vector<float>* err) override;
   // EncodeRGBToJpegData of the reference image, with the coefficients
   // computed on the device (and left resident as the originals).
   bool OriginalJpegData(JpegData* jpg);
@@ -182,9 +204,12 @@ class HipButteraugliComparator : public Comparator {
   std::string err_;
 };
 
-struct ProcessParams {  // guetzli::Params, processor.h:34-42 (4:4:4 subset)
+struct ProcessParams {  // guetzli::Params, processor.h:34-42
   float butteraugli_target = 1.0f;
   bool clear_metadata = true;
+  bool try_420 = false;
+  bool force_420 = false;
+  bool use_silver_screen = false;
   int zeroing_greedy_lookahead = 3;
   bool new_zeroing_model = true;
 };
@@ -209,8 +234,8 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
 
 // guetzli::Process(params, stats, jpeg_bytes, out) (processor.cc:1029-1066):
 // ReadJpeg, CheckJpegSanity, DecodeJpegToRGB as the comparator's reference,
-// ProcessJpegData on the input's own coefficients.  4:4:4 YCbCr inputs;
-// 4:2:0 (the reference's downsampling path) returns GZ_ERR_UNSUPPORTED.
+// ProcessJpegData on the input's own coefficients.  4:4:4 and 4:2:0 YCbCr
+// inputs (a 4:2:0 input forces the downsampled search).
 int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, size_t len,
                 ProcessResult* result, std::string* err);
 

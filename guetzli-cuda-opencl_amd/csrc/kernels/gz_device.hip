@@ -28,6 +28,7 @@ __constant__ GzTables c_tab;
 #include "butteraugli_kernels.inc"
 #include "scan_kernels.inc"
 #include "block_zeroing.inc"
+#include "block_zeroing420.inc"
 #include "coeff_kernels.inc"
 #include "jpeg_kernels.inc"
 
@@ -563,10 +564,11 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
+  if (compare_graph420_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph420_));
   if (stage_event_) hipEventDestroy(static_cast<hipEvent_t>(stage_event_));
   if (h_block_max_) hipHostFree(h_block_max_);
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
@@ -622,6 +624,7 @@ bool Engine::ComputeOriginalCoeffs(int16_t* host_out) {
 bool Engine::UploadCoeffs(const int16_t* coeffs) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  mode420_ = false;
   GZ_HIP(hipMemcpyAsync(d_cur_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
                         hipMemcpyHostToDevice, s));
   return true;
@@ -630,6 +633,7 @@ bool Engine::UploadCoeffs(const int16_t* coeffs) {
 bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  mode420_ = false;
   if (n == 0) return true;
   // the previous delta's kernel may still read the pinned staging
   GZ_HIP(hipStreamSynchronize(s));
@@ -657,6 +661,7 @@ bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n)
 bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  mode420_ = false;
   QuantMatrix qm;
   memcpy(qm.q, q, sizeof(qm.q));
   const size_t per = static_cast<size_t>(nb_) * 64;
@@ -716,7 +721,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
   }
   // S0: candidate coefficients -> linear RGB
-  GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_cur_, w_, h_, bw_, nb_, d_lin_));
+  GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(
+      d_cur_, w_, h_, bw_, nb_, d_lin_, mode420_ ? d_planes_ : nullptr));
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
   // S1-S3: opsin dynamics (blur + transform) and high intensity change
   // masking, fused
@@ -849,7 +855,8 @@ bool Engine::CompareEnqueue() {
   if (g_prof_on.load()) {
     if (!EnqueueCompare(nullptr)) return false;
   } else {
-    if (!compare_graph_) {
+    void*& graph = mode420_ ? compare_graph420_ : compare_graph_;
+    if (!graph) {
       hipGraph_t g = nullptr;
       GZ_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       const bool ok = EnqueueCompare(nullptr);
@@ -863,9 +870,9 @@ bool Engine::CompareEnqueue() {
       const hipError_t inst = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
       hipGraphDestroy(g);
       GZ_HIP(inst);
-      compare_graph_ = exec;
+      graph = exec;
     }
-    GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(compare_graph_), s));
+    GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graph), s));
   }
   GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
   return true;
@@ -968,7 +975,8 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
   if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
-                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
+                                     nullptr));
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
@@ -985,13 +993,22 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
   if (!OrderBlocks(comp_mask)) return false;
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
-                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_));
-  if (!ScanCounts(d_zero_count_, nb_, d_zero_off_, "scan_counts")) return false;
-  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nb_ + 3) / 4, 256, 0, s>>>(
-      static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nb_, limit, d_cand_idx_, d_cand_err_));
-  GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nb_ + 1) * 4, hipMemcpyDeviceToHost, s));
+                                     static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
+                                     nullptr));
+  return CompactCandidates(nb_, limit, offsets, idx, err);
+}
+
+// The kept entries of the first nblocks blocks' orders (d_zero_out_ /
+// d_zero_count_), concatenated, to the host.
+bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
+                               std::vector<uint8_t>* idx, std::vector<float>* err) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (!ScanCounts(d_zero_count_, nblocks, d_zero_off_, "scan_counts")) return false;
+  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nblocks + 3) / 4, 256, 0, s>>>(
+      static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nblocks, limit, d_cand_idx_, d_cand_err_));
+  GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nblocks + 1) * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
-  const size_t total = static_cast<size_t>(h_zero_off_[nb_]);
+  const size_t total = static_cast<size_t>(h_zero_off_[nblocks]);
   if (total > h_cand_cap_) {
     if (h_cand_idx_) GZ_HIP(hipHostFree(h_cand_idx_));
     if (h_cand_err_) GZ_HIP(hipHostFree(h_cand_err_));
@@ -1009,9 +1026,75 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
     GZ_HIP(hipStreamSynchronize(s));
   }
   ProfFlush();
-  offsets->assign(h_zero_off_, h_zero_off_ + nb_ + 1);
+  offsets->assign(h_zero_off_, h_zero_off_ + nblocks + 1);
   idx->assign(h_cand_idx_, h_cand_idx_ + total);
   err->assign(h_cand_err_, h_cand_err_ + total);
+  return true;
+}
+
+bool Engine::SetOriginal420(const int16_t* y, const int16_t* cb, const int16_t* cr) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  cbw_ = (w_ + 15) / 16;
+  cbh_ = (h_ + 15) / 16;
+  const size_t per = static_cast<size_t>(nb_) * 64, cper = static_cast<size_t>(cbw_) * cbh_ * 64;
+  GZ_HIP(hipMemcpyAsync(d_orig_, y, per * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_orig_ + per, cb, cper * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_orig_ + 2 * per, cr, cper * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::Set420(const int16_t* y, const int16_t* cb, const int16_t* cr, const uint16_t* plane_cb,
+                    const uint16_t* plane_cr) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  cbw_ = (w_ + 15) / 16;
+  cbh_ = (h_ + 15) / 16;
+  if (!d_planes_) GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_planes_), 2 * n_ * sizeof(uint16_t)));
+  const size_t per = static_cast<size_t>(nb_) * 64, cper = static_cast<size_t>(cbw_) * cbh_ * 64;
+  // (pageable sources: the copies are done when the calls return)
+  GZ_HIP(hipMemcpyAsync(d_cur_, y, per * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_cur_ + per, cb, cper * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_cur_ + 2 * per, cr, cper * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_planes_, plane_cb, n_ * 2, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_planes_ + n_, plane_cr, n_ * 2, hipMemcpyHostToDevice, s));
+  mode420_ = true;
+  return true;
+}
+
+bool Engine::BlockZeroingCandidates420(int comp_mask, float limit, int lookahead, bool new_model,
+                                       std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                                       std::vector<float>* err, uint16_t* plane_cb,
+                                       uint16_t* plane_cr) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!mode420_) return Fail("BlockZeroingCandidates420 without Set420", 0);
+  if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  if (comp_mask == 1) {
+    if (!OrderBlocks(1)) return false;
+    GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(
+        d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_, 1, limit, lookahead, new_model ? 1 : 0,
+        static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_, d_planes_));
+    return CompactCandidates(nb_, limit, offsets, idx, err);
+  }
+  if (comp_mask != 6) return Fail("BlockZeroingCandidates420 comp_mask", 0);
+  // wavefronts t = bx + 2 by (block_zeroing420.inc); by in
+  // [max(0, ceil((t - cbw + 1) / 2)), min(cbh - 1, t / 2)]
+  ProfBegin("block_zeroing420");
+  for (int t = 0; t <= (cbw_ - 1) + 2 * (cbh_ - 1); ++t) {
+    const int lo = std::max(0, (t - (cbw_ - 1) + 1) / 2), hi = std::min(cbh_ - 1, t / 2);
+    if (lo > hi) continue;
+    k_block_zeroing420<<<hi - lo + 1, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+                                                  cbw_, t, lo, limit, lookahead, new_model ? 1 : 0, d_planes_,
+                                                  static_cast<CoeffData*>(d_zero_out_), d_zero_count_);
+    GZ_HIP(hipGetLastError());
+  }
+  ProfEnd();
+  if (!CompactCandidates(cbw_ * cbh_, limit, offsets, idx, err)) return false;
+  GZ_HIP(hipMemcpyAsync(plane_cb, d_planes_, n_ * 2, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipMemcpyAsync(plane_cr, d_planes_ + n_, n_ * 2, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
   return true;
 }
 

@@ -399,6 +399,9 @@ __device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], c
 // ---------------------------------------------------------------------------
 
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+// ToPixels' byte of a 16-bit pixel value at column x (output_image.cc:83:
+// (p + 8 - (x & 1)) >> 4, stored as uint8_t)
+__device__ __forceinline__ int pixel_byte(unsigned p, int x) { return ((p + 8 - (x & 1)) >> 4) & 0xff; }
 
 // libjpeg build_ycc_rgb_table fixed-point factors FIX(x) = int(x * 2^16 + 0.5)
 // (color_transform.h tables): 1.40200, 1.77200, 0.71414, 0.34414.

@@ -67,6 +67,8 @@ class Engine {
   // An operation on this engine failed: it is not returned to the pool.
   bool failed() const { return failed_; }
   int blocks() const { return nb_; }
+  int block_w() const { return bw_; }
+  int block_h() const { return bh_; }
 
   // Reference image (RGB8 interleaved); computes and caches its XYB.
   bool SetReference(const uint8_t* rgb, bool device_ptr);
@@ -106,6 +108,24 @@ class Engine {
   // err[i] receives CompareBlock's double (the comparator-level adapter's
   // per-block entry; the search itself uses the batched calls above).
   bool CompareBlocks(int n, const int* blocks, const int16_t* cand, double* err);
+
+  // ---- the 4:2:0 pass (Params::try_420 / force_420, 4:2:0 input) ----
+  // Coefficients: Y at component 0 with luma block indices (blocks()), Cb /
+  // Cr at components 1 / 2 with chroma block indices (ceil(w/16) x
+  // ceil(h/16) blocks); the chroma pixels are the factor-2 planes' state
+  // (16-bit, [w*h] each), uploaded by the host.  Set420 switches the engine
+  // to it (Compare then reads the chroma pixels from the planes) until the
+  // next 4:4:4 upload / quantization.
+  bool SetOriginal420(const int16_t* y, const int16_t* cb, const int16_t* cr);
+  bool Set420(const int16_t* y, const int16_t* cb, const int16_t* cr, const uint16_t* plane_cb,
+              const uint16_t* plane_cr);
+  // The zeroing search of the 4:2:0 pass: comp_mask 1 (Y, with the chroma
+  // planes as they are) or 6 (Cb + Cr at factor 2, in wavefronts; the
+  // planes' state after the search comes back in plane_cb / plane_cr).
+  // Output as BlockZeroingCandidates, over the searched component's blocks.
+  bool BlockZeroingCandidates420(int comp_mask, float limit, int lookahead, bool new_model,
+                                 std::vector<int>* offsets, std::vector<uint8_t>* idx,
+                                 std::vector<float>* err, uint16_t* plane_cb, uint16_t* plane_cr);
 
   // Device entropy coding of the current coefficients with quant q (the
   // per-iteration JPEG of the search).  JpegStage: quantized zigzag
@@ -157,7 +177,10 @@ class Engine {
   // d_mb_ first; false when the Compare pass's fused edge_mask made it).
   bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b, bool front = true);
   bool EnqueueCompare(CompareDebug* dbg);
+  bool CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
+                         std::vector<uint8_t>* idx, std::vector<float>* err);
   void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
+  void* compare_graph420_ = nullptr;  // ... with the chroma from d_planes_
   void* stage_event_ = nullptr;    // hipEvent_t: the staged histograms reached the host
 
   int device_ = 0;
@@ -168,6 +191,8 @@ class Engine {
   bool failed_ = false;
   size_t bytes_ = 0;
   bool have_mask_scale_ = false;
+  bool mode420_ = false;      // the current candidate is a 4:2:0 one (Set420)
+  int cbw_ = 0, cbh_ = 0;     // chroma blocks of the 4:2:0 pass
 
   // device buffers
   uint8_t* d_rgb_ = nullptr;
@@ -188,6 +213,7 @@ class Engine {
   float* d_resval_ = nullptr;
   float* d_dd_ = nullptr;
   float* d_block_max_ = nullptr;
+  uint16_t* d_planes_ = nullptr;   // 4:2:0: Cb / Cr pixel state [2][w*h] (allocated on first use)
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
   int* d_zero_count_ = nullptr;    // [blocks] kept entries per block

@@ -322,7 +322,8 @@ def process(rgb, width, height, params=None, device=0, return_stats=False):
 
 def process_jpeg(jpeg, params=None, device=0, return_stats=False):
     """guetzli::Process on JPEG file bytes (processor.cc:1029-1066) -> JPEG
-    bytes.  4:4:4 YCbCr inputs; others raise GuetzliError(GZ_ERR_UNSUPPORTED)."""
+    bytes.  4:4:4 and 4:2:0 YCbCr inputs (4:2:0 forces the downsampled
+    search); others raise GuetzliError(GZ_ERR_UNSUPPORTED)."""
     L = lib()
     buf = ctypes.create_string_buffer(bytes(jpeg), len(jpeg))
     p = (params or Params())._c()

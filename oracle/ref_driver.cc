@@ -93,6 +93,7 @@ int Encode(int argc, char** argv) {
   params.butteraugli_target =
       static_cast<float>(guetzli::ButteraugliScoreForQuality(quality));
   // optional Params overrides: lookahead=N new_model=0|1 try_420=0|1 force_420=0|1
+  // silver=0|1 (use_silver_screen)
   for (int i = 8; i < argc; ++i) {
     const std::string kv = argv[i];
     const size_t eq = kv.find('=');
@@ -103,6 +104,7 @@ int Encode(int argc, char** argv) {
     else if (k == "new_model") params.new_zeroing_model = v != 0;
     else if (k == "try_420") params.try_420 = v != 0;
     else if (k == "force_420") params.force_420 = v != 0;
+    else if (k == "silver") params.use_silver_screen = v != 0;
     else return 1;
   }
   guetzli::ProcessStats stats;

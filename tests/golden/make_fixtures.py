@@ -148,6 +148,29 @@ def main():
             ("tex_100x77_q95_oldmodel", tex, 100, 77, 95, {"new_model": 0}),
             ("tex_100x77_q95_lookahead2", tex, 100, 77, 95, {"lookahead": 2}),
         ], section="e2e_params")
+    if "e2e-420" in what:
+        # the 4:2:0 pass (Params::try_420 / force_420 / use_silver_screen,
+        # processor.cc:986-1016): downsampled search alone, both passes, the
+        # silver-screen downsampler, odd sizes (partial 16x16 chroma blocks)
+        bees = os.path.join(HERE, "bees.rgb")
+
+        def stage(name):
+            d = os.path.join(HERE, "stages_" + name)
+            meta = dict(l.split() for l in open(os.path.join(d, "meta.txt")) if len(l.split()) == 2)
+            return os.path.join(d, "input.rgb"), int(meta["w"]), int(meta["h"])
+
+        cases = [("bees_q95_force420", bees, 444, 258, 95, {"force_420": 1}),
+                 ("bees_q90_try420", bees, 444, 258, 90, {"try_420": 1}),
+                 ("bees_q95_force420_silver", bees, 444, 258, 95, {"force_420": 1, "silver": 1})]
+        for name, q, params in [("tex_64x48", 95, {"force_420": 1}), ("tex_100x77", 95, {"force_420": 1}),
+                                ("tex_41x33", 95, {"force_420": 1}), ("bees_88x64", 95, {"try_420": 1}),
+                                ("tex_100x77", 90, {"force_420": 1, "new_model": 0}),
+                                ("tex_64x48", 95, {"force_420": 1, "lookahead": 1})]:
+            rgb, w, h = stage(name)
+            tag = "_".join("%s%d" % kv for kv in sorted(params.items()) if kv[0] not in ("force_420", "try_420"))
+            cases.append(("%s_q%d_%s%s" % (name, q, "try420" if "try_420" in params else "force420",
+                                           "_" + tag if tag else ""), rgb, w, h, q, params))
+        run_e2e(manifest, cases, section="e2e_420")
     json.dump(manifest, open(manifest_path, "w"), indent=1, sort_keys=True)
 
 

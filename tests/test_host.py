@@ -147,7 +147,7 @@ def test_bad_arguments_fail_loudly(gz):
     with pytest.raises(gz.GuetzliError):
         gz.rgb_to_coeffs(np.zeros(10, np.uint8), 4, 4)
     with pytest.raises(gz.GuetzliError):
-        gz.process(np.zeros(3 * 64 * 64, np.uint8), 64, 64, gz.Params(try_420=True))
+        gz.process(np.zeros(3 * 64 * 64, np.uint8), 64, 64, gz.Params(butteraugli_target=3.0))
 
 
 def test_no_cpu_fallback_without_gpu(gz, gpu_available):

@@ -62,21 +62,15 @@ def test_reader_rejects_invalid_input(bad):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", sorted(n for n in CASES if "_420" not in n and CASES[n]["reference_ok"]))
+@pytest.mark.parametrize("name", sorted(n for n in CASES if CASES[n]["reference_ok"]))
 def test_process_jpeg_matches_reference(name):
     e = CASES[name]
     assert e["reference_ok"]
     params = gz.Params.for_quality(e["quality"], clear_metadata=e.get("clear_metadata", True))
     out, st = gz.process_jpeg(_data(name), params, return_stats=True)
+    assert st.iterations == e["iters"]
     assert len(out) == e["bytes"]
     assert _sha(out) == e["sha256"]
-
-
-@pytest.mark.gpu
-def test_process_jpeg_420_is_unsupported():
-    with pytest.raises(gz.GuetzliError) as ei:
-        gz.process_jpeg(_data("synth_pil_q85_420"), gz.Params.for_quality(95))
-    assert ei.value.status == 4  # GZ_ERR_UNSUPPORTED
 
 
 @pytest.mark.gpu
