@@ -41,8 +41,12 @@ void HipButteraugliComparator::Compare(const OutputImage& img) {
   if (img.width() != width_ || img.height() != height_) Die("Compare: image size");
   for (int c = 0; c < 3; ++c) {
     const OutputImageComponent& comp = img.component(c);
-    if (comp.factor_x() != 1 || comp.factor_y() != 1)
-      Die("Compare: subsampled component (4:2:0 is not supported by this adapter)");
+    if (comp.factor_x() != 1 || comp.factor_y() != 1) {
+      // subsampled: the pixels (ToLinearRGB's source) are the input
+      const std::vector<uint8_t> rgb = img.ToSRGB();
+      if (gz_comparator_compare_rgb(cmp_, rgb.data(), &distance_) != GZ_OK) Die("Compare");
+      return;
+    }
     // [blocks][64] per component: the layout of OutputImageComponent::coeffs()
     memcpy(&coeffs_[static_cast<size_t>(c) * num_blocks_ * 64], comp.coeffs(),
            static_cast<size_t>(num_blocks_) * 64 * sizeof(coeff_t));
@@ -57,15 +61,28 @@ void HipButteraugliComparator::StartBlockComparisons() {
 
 void HipButteraugliComparator::SwitchBlock(int block_x, int block_y, int factor_x,
                                            int factor_y) {
-  if (factor_x != 1 || factor_y != 1)
-    Die("SwitchBlock: factor != 1 (4:2:0 is not supported by this adapter)");
   block_x_ = block_x;
   block_y_ = block_y;
+  factor_x_ = factor_x;
+  factor_y_ = factor_y;
 }
 
 double HipButteraugliComparator::CompareBlock(const OutputImage& img, int off_x, int off_y,
                                               const coeff_t* candidate_block,
                                               const int comp_mask) const {
+  bool subsampled = factor_x_ != 1 || factor_y_ != 1;
+  for (int c = 0; c < 3; ++c)
+    subsampled = subsampled || img.component(c).factor_x() != 1 || img.component(c).factor_y() != 1;
+  if (subsampled) {
+    // (also the Y search of a 4:2:0 image: its chroma pixels are state)
+    // the 8x8 block (block_x * factor_x + off_x, ...) as ToLinearRGB reads it
+    const int bx = block_x_ * factor_x_ + off_x, by = block_y_ * factor_y_ + off_y;
+    const std::vector<uint8_t> rgb = img.ToSRGB(8 * bx, 8 * by, 8, 8);
+    const int b = by * block_width_ + bx;
+    double err = 0.0;
+    if (gz_comparator_compare_blocks_rgb(cmp_, 1, &b, rgb.data(), &err) != GZ_OK) Die("CompareBlock");
+    return err;
+  }
   if (off_x != 0 || off_y != 0) Die("CompareBlock: offset within a 4:4:4 block");
   for (int c = 0; c < 3; ++c) {
     if (comp_mask & (1 << c)) {

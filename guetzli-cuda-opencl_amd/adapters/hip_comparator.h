@@ -10,8 +10,10 @@
 // aborts with a message (the Comparator interface has no error channel, and
 // there is no CPU fallback).
 //
-// Scope: 4:4:4 images (every component factor 1).  SwitchBlock with a factor
-// other than 1 (the reference's 4:2:0 search) aborts with a message.
+// Images with subsampled components (the reference's 4:2:0 search): their
+// pixels are state of the OutputImage, not a function of the coefficients,
+// so Compare / CompareBlock send the image's sRGB pixels (ToSRGB) instead of
+// its coefficients (gz_comparator_compare_rgb / _compare_blocks_rgb).
 #ifndef GUETZLI_HIP_ADAPTER_HIP_COMPARATOR_H_
 #define GUETZLI_HIP_ADAPTER_HIP_COMPARATOR_H_
 
@@ -35,7 +37,8 @@ class HipButteraugliComparator : public Comparator {
   ~HipButteraugliComparator() override;
 
   // Comparator::Compare (butteraugli_comparator.cc:60-70): the image's DCT
-  // coefficients go to the device; distance + per-block maxima come back.
+  // coefficients (4:4:4) or its sRGB pixels (subsampled components) go to
+  // the device; distance + per-block maxima come back.
   void Compare(const OutputImage& img) override;
   // butteraugli_comparator.cc:72-83: the activity mask of the reference.
   void StartBlockComparisons() override;
@@ -44,7 +47,10 @@ class HipButteraugliComparator : public Comparator {
   // formed on the device per CompareBlock call).
   void SwitchBlock(int block_x, int block_y, int factor_x, int factor_y) override;
   // butteraugli_comparator.cc:113-163 on the device: `candidate_block` for
-  // the components in comp_mask, the image's current block for the others.
+  // the components in comp_mask, the image's current block for the others
+  // (4:4:4); the image's 8x8 sRGB window at the block when img has
+  // subsampled components (the caller has set the candidate into img,
+  // processor.cc:426-431).
   double CompareBlock(const OutputImage& img, int off_x, int off_y,
                       const coeff_t* candidate_block, const int comp_mask) const override;
   // butteraugli_comparator.cc:235-237
@@ -68,7 +74,7 @@ class HipButteraugliComparator : public Comparator {
   const int width_, height_, block_width_, num_blocks_;
   const float target_;
   float distance_ = 0.0f;
-  int block_x_ = 0, block_y_ = 0;
+  int block_x_ = 0, block_y_ = 0, factor_x_ = 1, factor_y_ = 1;
   std::vector<int16_t> coeffs_;  // [3][blocks][64] staging of Compare
   mutable std::vector<int16_t> cand_;  // [3][64] staging of CompareBlock
 };

@@ -39,7 +39,8 @@ struct gz_comparator {
   float distance = 0.0f;
   int w = 0, h = 0;
   std::vector<float> block_max;
-  std::vector<int16_t> last;  // coefficients of the last compare (distmap())
+  std::vector<int16_t> last;      // coefficients of the last compare (distmap())
+  std::vector<uint8_t> last_rgb;  // ... or its sRGB pixels (gz_comparator_compare_rgb)
 };
 
 extern "C" {
@@ -116,6 +117,19 @@ static gz_status CompareImpl(gz_comparator* cmp, const int16_t* coeffs, gz::Comp
   if (!e.UploadCoeffs(coeffs) || !e.Compare(&cmp->distance, cmp->block_max.data(), dbg))
     return SetError(GZ_ERR_DEVICE, "compare: " + e.error());
   cmp->last.assign(coeffs, coeffs + static_cast<size_t>(e.blocks()) * 192);
+  cmp->last_rgb.clear();
+  if (distance) *distance = cmp->distance;
+  return GZ_OK;
+}
+
+gz_status gz_comparator_compare_rgb(gz_comparator* cmp, const uint8_t* rgb, float* distance) {
+  if (!cmp || !rgb) return SetError(GZ_ERR_INVALID_ARG, "compare_rgb: bad argument");
+  gz::Engine& e = *cmp->engine;
+  cmp->block_max.resize(e.blocks());
+  if (!e.SetCandidateRgb(rgb) || !e.Compare(&cmp->distance, cmp->block_max.data(), nullptr))
+    return SetError(GZ_ERR_DEVICE, "compare_rgb: " + e.error());
+  cmp->last_rgb.assign(rgb, rgb + static_cast<size_t>(3) * cmp->w * cmp->h);
+  cmp->last.clear();
   if (distance) *distance = cmp->distance;
   return GZ_OK;
 }
@@ -146,15 +160,16 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
 
 gz_status gz_comparator_distmap(gz_comparator* cmp, float* out) {
   if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "distmap: bad argument");
-  if (cmp->last.empty()) return SetError(GZ_ERR_INVALID_ARG, "distmap: no compare yet");
+  if (cmp->last.empty() && cmp->last_rgb.empty())
+    return SetError(GZ_ERR_INVALID_ARG, "distmap: no compare yet");
   gz::Engine& e = *cmp->engine;
   // the pass again on the same candidate, with the map read back (the
   // search's passes keep only the per-block maxima)
   gz::CompareDebug dbg;
   dbg.distmap = out;
   float d = 0.0f;
-  if (!e.UploadCoeffs(cmp->last.data()) || !e.Compare(&d, nullptr, &dbg))
-    return SetError(GZ_ERR_DEVICE, "distmap: " + e.error());
+  const bool up = cmp->last.empty() ? e.SetCandidateRgb(cmp->last_rgb.data()) : e.UploadCoeffs(cmp->last.data());
+  if (!up || !e.Compare(&d, nullptr, &dbg)) return SetError(GZ_ERR_DEVICE, "distmap: " + e.error());
   return GZ_OK;
 }
 
@@ -168,6 +183,19 @@ gz_status gz_comparator_compare_blocks(gz_comparator* cmp, int n, const int* blo
       return SetError(GZ_ERR_INVALID_ARG, "compare_blocks: block index out of range");
   if (!e.CompareBlocks(n, blocks, cand, err))
     return SetError(GZ_ERR_DEVICE, "compare_blocks: " + e.error());
+  return GZ_OK;
+}
+
+gz_status gz_comparator_compare_blocks_rgb(gz_comparator* cmp, int n, const int* blocks,
+                                           const uint8_t* rgb, double* err) {
+  if (!cmp || n < 0 || (n > 0 && (!blocks || !rgb || !err)))
+    return SetError(GZ_ERR_INVALID_ARG, "compare_blocks_rgb: bad argument");
+  gz::Engine& e = *cmp->engine;
+  for (int i = 0; i < n; ++i)
+    if (blocks[i] < 0 || blocks[i] >= e.blocks())
+      return SetError(GZ_ERR_INVALID_ARG, "compare_blocks_rgb: block index out of range");
+  if (!e.CompareBlocksRgb(n, blocks, rgb, err))
+    return SetError(GZ_ERR_DEVICE, "compare_blocks_rgb: " + e.error());
   return GZ_OK;
 }
 

@@ -564,11 +564,11 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (compare_graph_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph_));
-  if (compare_graph420_) hipGraphExecDestroy(static_cast<hipGraphExec_t>(compare_graph420_));
+  for (void* g : compare_graph_)
+    if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
   if (stage_event_) hipEventDestroy(static_cast<hipEvent_t>(stage_event_));
   if (h_block_max_) hipHostFree(h_block_max_);
   if (h_delta_idx_) hipHostFree(h_delta_idx_);
@@ -624,7 +624,7 @@ bool Engine::ComputeOriginalCoeffs(int16_t* host_out) {
 bool Engine::UploadCoeffs(const int16_t* coeffs) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  mode420_ = false;
+  cand_src_ = kCandCoeffs;
   GZ_HIP(hipMemcpyAsync(d_cur_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
                         hipMemcpyHostToDevice, s));
   return true;
@@ -633,7 +633,7 @@ bool Engine::UploadCoeffs(const int16_t* coeffs) {
 bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  mode420_ = false;
+  cand_src_ = kCandCoeffs;
   if (n == 0) return true;
   // the previous delta's kernel may still read the pinned staging
   GZ_HIP(hipStreamSynchronize(s));
@@ -661,7 +661,7 @@ bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n)
 bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  mode420_ = false;
+  cand_src_ = kCandCoeffs;
   QuantMatrix qm;
   memcpy(qm.q, q, sizeof(qm.q));
   const size_t per = static_cast<size_t>(nb_) * 64;
@@ -721,8 +721,12 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
   }
   // S0: candidate coefficients -> linear RGB
-  GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(
-      d_cur_, w_, h_, bw_, nb_, d_lin_, mode420_ ? d_planes_ : nullptr));
+  if (cand_src_ == kCandRgb) {
+    GZ_TIMED("rgb_to_linear", k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_cand_rgb_, n_, d_lin_));
+  } else {
+    GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(
+        d_cur_, w_, h_, bw_, nb_, d_lin_, cand_src_ == kCand420 ? d_planes_ : nullptr));
+  }
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
   // S1-S3: opsin dynamics (blur + transform) and high intensity change
   // masking, fused
@@ -855,7 +859,7 @@ bool Engine::CompareEnqueue() {
   if (g_prof_on.load()) {
     if (!EnqueueCompare(nullptr)) return false;
   } else {
-    void*& graph = mode420_ ? compare_graph420_ : compare_graph_;
+    void*& graph = compare_graph_[cand_src_];
     if (!graph) {
       hipGraph_t g = nullptr;
       GZ_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -933,6 +937,47 @@ bool Engine::CompareBlocks(int n, const int* blocks, const int16_t* cand, double
   GZ_HIP(hipMemcpyAsync(d_cand, cand, static_cast<size_t>(n) * 384, hipMemcpyHostToDevice, s));
   GZ_TIMED("compare_blocks", k_compare_blocks<<<n, 64, 0, s>>>(d_blocks, d_cand, n, d_rgb_, d_mask_scale_,
                                                                 w_, h_, bw_, d_err));
+  GZ_HIP(hipMemcpyAsync(err, d_err, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  return true;
+}
+
+bool Engine::SetCandidateRgb(const uint8_t* rgb) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!d_cand_rgb_) GZ_HIP(hipMalloc(reinterpret_cast<void**>(&d_cand_rgb_), 3 * n_));
+  GZ_HIP(hipMemcpyAsync(d_cand_rgb_, rgb, 3 * n_, hipMemcpyHostToDevice, s));
+  cand_src_ = kCandRgb;
+  return true;
+}
+
+bool Engine::CompareBlocksRgb(int n, const int* blocks, const uint8_t* rgb, double* err) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (n <= 0) return true;
+  for (int i = 0; i < n; ++i)
+    if (blocks[i] < 0 || blocks[i] >= nb_) return Fail("CompareBlocksRgb block index", 0);
+  if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
+  // one staging buffer: block indices | windows | errors
+  const size_t need = static_cast<size_t>(n) * (4 + 192 + 8) + 64;
+  if (need > cbreq_cap_) {
+    GZ_HIP(hipStreamSynchronize(s));
+    if (d_cbreq_) GZ_HIP(hipFree(d_cbreq_));
+    d_cbreq_ = nullptr;
+    cbreq_cap_ = 0;
+    GZ_HIP(hipMalloc(&d_cbreq_, need));
+    cbreq_cap_ = need;
+  }
+  char* base = static_cast<char*>(d_cbreq_);
+  int* d_blocks = reinterpret_cast<int*>(base);
+  uint8_t* d_rgb = reinterpret_cast<uint8_t*>(base + ((static_cast<size_t>(n) * 4 + 15) & ~15ull));
+  double* d_err = reinterpret_cast<double*>(
+      reinterpret_cast<char*>(d_rgb) + ((static_cast<size_t>(n) * 192 + 15) & ~15ull));
+  GZ_HIP(hipMemcpyAsync(d_blocks, blocks, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(d_rgb, rgb, static_cast<size_t>(n) * 192, hipMemcpyHostToDevice, s));
+  GZ_TIMED("compare_blocks_rgb", k_compare_blocks_rgb<<<n, 64, 0, s>>>(d_blocks, d_rgb, n, d_rgb_, d_mask_scale_,
+                                                                        w_, h_, bw_, d_err));
   GZ_HIP(hipMemcpyAsync(err, d_err, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
@@ -1059,7 +1104,7 @@ bool Engine::Set420(const int16_t* y, const int16_t* cb, const int16_t* cr, cons
   GZ_HIP(hipMemcpyAsync(d_cur_ + 2 * per, cr, cper * 2, hipMemcpyHostToDevice, s));
   GZ_HIP(hipMemcpyAsync(d_planes_, plane_cb, n_ * 2, hipMemcpyHostToDevice, s));
   GZ_HIP(hipMemcpyAsync(d_planes_ + n_, plane_cr, n_ * 2, hipMemcpyHostToDevice, s));
-  mode420_ = true;
+  cand_src_ = kCand420;
   return true;
 }
 
@@ -1069,7 +1114,7 @@ bool Engine::BlockZeroingCandidates420(int comp_mask, float limit, int lookahead
                                        uint16_t* plane_cr) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
-  if (!mode420_) return Fail("BlockZeroingCandidates420 without Set420", 0);
+  if (cand_src_ != kCand420) return Fail("BlockZeroingCandidates420 without Set420", 0);
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (comp_mask == 1) {
     if (!OrderBlocks(1)) return false;

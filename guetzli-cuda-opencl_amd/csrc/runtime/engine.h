@@ -127,6 +127,13 @@ class Engine {
                                  std::vector<int>* offsets, std::vector<uint8_t>* idx,
                                  std::vector<float>* err, uint16_t* plane_cb, uint16_t* plane_cr);
 
+  // ---- candidates given as pixels (the comparator-level drop-in for any
+  // OutputImage, subsampled components included) ----
+  // The next Compare reads the candidate as sRGB (3*w*h bytes, ToSRGB).
+  bool SetCandidateRgb(const uint8_t* rgb);
+  // CompareBlock of n requests with 8x8 sRGB windows rgb[192 * i ..].
+  bool CompareBlocksRgb(int n, const int* blocks, const uint8_t* rgb, double* err);
+
   // Device entropy coding of the current coefficients with quant q (the
   // per-iteration JPEG of the search).  JpegStage: quantized zigzag
   // coefficients, symbol histograms hist[comp*2 + {0:DC, 1:AC}][256] (plain
@@ -179,8 +186,10 @@ class Engine {
   bool EnqueueCompare(CompareDebug* dbg);
   bool CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
                          std::vector<uint8_t>* idx, std::vector<float>* err);
-  void* compare_graph_ = nullptr;  // hipGraphExec_t of EnqueueCompare(nullptr)
-  void* compare_graph420_ = nullptr;  // ... with the chroma from d_planes_
+  // what Compare's first stage reads (and its hipGraphExec_t each)
+  enum CandSource { kCandCoeffs = 0, kCand420 = 1, kCandRgb = 2 };
+  int cand_src_ = kCandCoeffs;
+  void* compare_graph_[3] = {nullptr, nullptr, nullptr};
   void* stage_event_ = nullptr;    // hipEvent_t: the staged histograms reached the host
 
   int device_ = 0;
@@ -191,7 +200,6 @@ class Engine {
   bool failed_ = false;
   size_t bytes_ = 0;
   bool have_mask_scale_ = false;
-  bool mode420_ = false;      // the current candidate is a 4:2:0 one (Set420)
   int cbw_ = 0, cbh_ = 0;     // chroma blocks of the 4:2:0 pass
 
   // device buffers
@@ -214,6 +222,7 @@ class Engine {
   float* d_dd_ = nullptr;
   float* d_block_max_ = nullptr;
   uint16_t* d_planes_ = nullptr;   // 4:2:0: Cb / Cr pixel state [2][w*h] (allocated on first use)
+  uint8_t* d_cand_rgb_ = nullptr;  // sRGB candidate [3*w*h] (allocated on first use)
   float* d_mask_scale_ = nullptr;
   void* d_zero_out_ = nullptr;
   int* d_zero_count_ = nullptr;    // [blocks] kept entries per block

@@ -78,7 +78,8 @@ EXPORTED_SYMBOLS = (
     "gz_profile_enable", "gz_profile_reset", "gz_profile_get", "gz_profile_names",
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
     "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode", "gz_comparator_distmap",
-    "gz_comparator_compare_blocks", "gz_png_decode",
+    "gz_comparator_compare_blocks", "gz_png_decode", "gz_comparator_compare_rgb",
+    "gz_comparator_compare_blocks_rgb",
 )
 
 _lib = None

@@ -49,7 +49,9 @@ typedef struct {
 } gz_coeff_data;
 
 /* guetzli::Params (guetzli/processor.h:34-42); same defaults via
- * gz_params_init().  try_420 / force_420 are not supported (GZ_ERR_UNSUPPORTED). */
+ * gz_params_init().  try_420 / force_420 / use_silver_screen run the 4:2:0
+ * pass of ProcessJpegData (processor.cc:986-1016); the strip decomposition of
+ * one frame (gz_process_rgb_strips) supports the 4:4:4 search only. */
 typedef struct {
   float butteraugli_target;
   int clear_metadata;
@@ -118,8 +120,9 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
  * (guetzli/processor.h:44-46, processor.cc:1029-1066) -- the input's own
  * coefficients and quantization start the search, its decoded pixels are the
  * Butteraugli reference.  Baseline / extended / progressive Huffman JPEGs with
- * 4:4:4 YCbCr sampling; 4:2:0 and other layouts return GZ_ERR_UNSUPPORTED,
- * unreadable input GZ_ERR_INVALID_ARG.  *jpeg_out: library-allocated
+ * 4:4:4 or 4:2:0 YCbCr sampling (4:2:0 forces the downsampled search); other
+ * layouts and 1-component files return GZ_ERR_UNSUPPORTED (the reference's
+ * Process returns false for them), unreadable input GZ_ERR_INVALID_ARG.  *jpeg_out: library-allocated
  * (gz_free). */
 gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jpeg, size_t jpeg_len,
                           uint8_t** jpeg_out, size_t* jpeg_size, gz_process_stats* stats);
@@ -172,6 +175,11 @@ void gz_comparator_destroy(gz_comparator* cmp);
 /* Comparator::Compare (guetzli/butteraugli_comparator.cc:60-70) on the image
  * whose DCT coefficients are `coeffs`; distance = distmap_aggregate(). */
 gz_status gz_comparator_compare(gz_comparator* cmp, const int16_t* coeffs, float* distance);
+/* Comparator::Compare of an image given as its sRGB pixels (3*w*h bytes,
+ * RGB interleaved -- OutputImage::ToSRGB(), output_image.cc:654-701): the
+ * entry for images whose pixels are not a function of their coefficients
+ * alone (4:2:0: the subsampled components' upsampled pixels are state). */
+gz_status gz_comparator_compare_rgb(gz_comparator* cmp, const uint8_t* rgb, float* distance);
 /* Same, with stage dumps. */
 gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs,
                                        gz_compare_stages* stages, float* distance);
@@ -227,6 +235,13 @@ gz_status gz_comparator_block_zeroing_orders(gz_comparator* cmp, const int16_t* 
  * batched gz_comparator_block_zeroing_orders. */
 gz_status gz_comparator_compare_blocks(gz_comparator* cmp, int n, const int* blocks,
                                        const int16_t* cand, double* err);
+/* The same with each candidate given as its 8x8 sRGB window rgb[192*i ..]
+ * (row major, RGB interleaved, as OutputImage::ToSRGB(8 bx, 8 by, 8, 8)
+ * returns it, edge pixels replicated): CompareBlock(img, off_x, off_y, ...)
+ * of any image, subsampled components included (butteraugli_comparator.cc:
+ * 113-163 reads the image only through ToLinearRGB). */
+gz_status gz_comparator_compare_blocks_rgb(gz_comparator* cmp, int n, const int* blocks,
+                                           const uint8_t* rgb, double* err);
 
 /* SaveToJpegData + WriteJpeg (guetzli/output_image.cc:579-640,
  * jpeg_data_writer.cc:540-553) of dequantized coefficients `coeffs`

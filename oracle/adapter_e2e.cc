@@ -8,8 +8,9 @@
 // headers.  The GPU tests check both encodes against the reference's known
 // answers (tests/golden/manifest.json).
 //
-//   adapter_e2e comparator RGB W H QUALITY OUT.jpg   reference Processor + HIP comparator
-//   adapter_e2e process    RGB W H QUALITY OUT.jpg   ProcessHip (gz_process_rgb)
+//   adapter_e2e comparator RGB W H QUALITY OUT.jpg [k=v ...]  reference Processor + HIP comparator
+//   adapter_e2e process    RGB W H QUALITY OUT.jpg [k=v ...]  ProcessHip (gz_process_rgb)
+// k=v: Params overrides try_420 / force_420 / silver (use_silver_screen).
 //
 // Prints "iterations N" on success; exits 1 on a failed encode.
 
@@ -29,8 +30,8 @@
 #include "process_hip.h"
 
 int main(int argc, char** argv) {
-  if (argc != 7) {
-    fprintf(stderr, "usage: %s comparator|process RGB W H QUALITY OUT.jpg\n", argv[0]);
+  if (argc < 7) {
+    fprintf(stderr, "usage: %s comparator|process RGB W H QUALITY OUT.jpg [k=v ...]\n", argv[0]);
     return 2;
   }
   const std::string mode = argv[1];
@@ -46,6 +47,17 @@ int main(int argc, char** argv) {
   g_mathMode = MODE_CPU_OPT;  // the `guetzli --c` search loop (guetzli.cc)
   guetzli::Params params;
   params.butteraugli_target = static_cast<float>(guetzli::ButteraugliScoreForQuality(quality));
+  for (int i = 7; i < argc; ++i) {
+    const std::string kv = argv[i];
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) return 2;
+    const std::string k = kv.substr(0, eq);
+    const bool v = atoi(kv.c_str() + eq + 1) != 0;
+    if (k == "try_420") params.try_420 = v;
+    else if (k == "force_420") params.force_420 = v;
+    else if (k == "silver") params.use_silver_screen = v;
+    else return 2;
+  }
   guetzli::ProcessStats stats;
   std::string out;
   bool ok = false;

@@ -28,11 +28,12 @@ def _need_bin():
         pytest.skip("oracle/_ref/adapter_e2e not built (needs /root/reference at build time)")
 
 
-def _run(mode, name, tmp_path, timeout=600):
-    e = MANIFEST["e2e"][name]
+def _run(mode, name, tmp_path, timeout=600, section="e2e"):
+    e = MANIFEST[section][name]
     out = tmp_path / ("%s_%s.jpg" % (mode, name))
+    kv = ["%s=%d" % p for p in sorted(e.get("params", {}).items())]
     r = subprocess.run([BIN, mode, os.path.join(GOLDEN, e["input"]), str(e["w"]), str(e["h"]),
-                        str(e["quality"]), str(out)], capture_output=True, text=True,
+                        str(e["quality"]), str(out)] + kv, capture_output=True, text=True,
                        timeout=timeout)
     return e, out, r
 
@@ -53,6 +54,23 @@ def test_adapters_fail_loudly_without_gpu(gz, mode, tmp_path):
 def test_adapters_reproduce_reference(mode, name, tmp_path):
     _need_bin()
     e, out, r = _run(mode, name, tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["iterations", str(e["iters"])], r.stdout
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,name", [("comparator", "tex_64x48_q95_force420"),
+                                       ("comparator", "tex_41x33_q95_force420"),
+                                       ("process", "bees_q90_try420")])
+def test_adapters_reproduce_reference_420(mode, name, tmp_path):
+    """The 4:2:0 search: in comparator mode the reference's own factor-2
+    loop (SwitchBlock(.., 2, 2), CompareBlock at the four luma offsets, the
+    stateful SetCoeffBlock on the reference's OutputImage) drives the
+    comparator through the sRGB entries (gz_comparator_compare_rgb /
+    _compare_blocks_rgb)."""
+    _need_bin()
+    e, out, r = _run(mode, name, tmp_path, section="e2e_420")
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split() == ["iterations", str(e["iters"])], r.stdout
     assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
