@@ -516,4 +516,25 @@ __device__ __forceinline__ void real_fft8(const T* in, T* re, T* im, T sqrt_half
   fft_reorder8(re, im);
 }
 
+// True in every thread of the last workgroup to reach this point (all
+// threads of every workgroup must call it); *done counts arrivals and is
+// reset to 0 by the last one.  Only for data that every workgroup updates
+// and the last one reads with device-scope atomics (coherent across the
+// XCDs' L2s): the barrier waits for this workgroup's atomics to complete
+// before the arrival is counted.  No device-scope fence -- on gfx950 that
+// writes back the XCD's L2, which costs more than the whole kernel.
+__device__ __forceinline__ bool last_block_done(uint32_t* done) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = atomicAdd(done, 1u);
+    const bool last = prev == gridDim.x * gridDim.y * gridDim.z - 1;
+    if (last) atomicExch(done, 0u);
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
 }  // namespace gz
