@@ -984,6 +984,36 @@ bool Engine::CompareBlocksRgb(int n, const int* blocks, const uint8_t* rgb, doub
   return true;
 }
 
+// Diagnostics: with GZ_BZ_TRACE=path every zeroing search writes per block
+// (start, end, steps) -- 100 MHz wall clock, int64 -- to path (the last
+// search's, overwritten each time).
+static long long* BzTraceBuf(int nb, void* stream) {
+  static const char* path = getenv("GZ_BZ_TRACE");
+  if (!path) return nullptr;
+  static long long* buf = nullptr;
+  static int cap = 0;
+  if (nb > cap) {
+    if (buf) hipFree(buf);
+    buf = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), static_cast<size_t>(nb) * 24) != hipSuccess) return nullptr;
+    cap = nb;
+  }
+  (void)stream;
+  return buf;
+}
+static void BzTraceDump(long long* buf, int nb, void* stream) {
+  static const char* path = getenv("GZ_BZ_TRACE");
+  if (!buf || !path) return;
+  std::vector<long long> h(static_cast<size_t>(nb) * 3);
+  if (hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)) != hipSuccess ||
+      hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess)
+    return;
+  if (FILE* f = fopen(path, "wb")) {
+    fwrite(h.data(), 8, h.size(), f);
+    fclose(f);
+  }
+}
+
 // Debug knob (GZ_BZ_LDS_PAD bytes of unused dynamic LDS) to probe how the
 // zeroing search's speed depends on occupancy.
 static size_t BzLdsPad() {
@@ -1018,10 +1048,12 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
+  long long* tr = BzTraceBuf(nb_, stream_);
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
-                                     nullptr));
+                                     nullptr, tr));
+  BzTraceDump(tr, nb_, stream_);
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
@@ -1036,10 +1068,12 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
   GZ_HIP(hipSetDevice(device_));
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
+  long long* tr = BzTraceBuf(nb_, stream_);
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
-                                     nullptr));
+                                     nullptr, tr));
+  BzTraceDump(tr, nb_, stream_);
   return CompactCandidates(nb_, limit, offsets, idx, err);
 }
 
@@ -1120,7 +1154,7 @@ bool Engine::BlockZeroingCandidates420(int comp_mask, float limit, int lookahead
     if (!OrderBlocks(1)) return false;
     GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(
         d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_, 1, limit, lookahead, new_model ? 1 : 0,
-        static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_, d_planes_));
+        static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_, d_planes_, nullptr));
     return CompactCandidates(nb_, limit, offsets, idx, err);
   }
   if (comp_mask != 6) return Fail("BlockZeroingCandidates420 comp_mask", 0);

@@ -171,6 +171,16 @@ def main():
             cases.append(("%s_q%d_%s%s" % (name, q, "try420" if "try_420" in params else "force420",
                                            "_" + tag if tag else ""), rgb, w, h, q, params))
         run_e2e(manifest, cases, section="e2e_420")
+    if "e2e-420-1080" in what:
+        # the 4:2:0 pass at full size: synthetic 1920x1080 seed 0 (the bench's
+        # frame), q95, force_420 -- about 7 minutes of reference CPU time
+        sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+        import guetzli_amd as gz
+        rgb = "/tmp/gz_fixture_synth_1080_s0.rgb"
+        gz.synthetic_frame(0, 1920, 1080).tofile(rgb)
+        run_e2e(manifest, [("synth_1920x1080_s0_q95_force420", rgb, 1920, 1080, 95, {"force_420": 1})],
+                section="e2e_420")
+        manifest["e2e_420"]["synth_1920x1080_s0_q95_force420"]["input"] = "synthetic:0"
     json.dump(manifest, open(manifest_path, "w"), indent=1, sort_keys=True)
 
 

@@ -50,8 +50,9 @@ def test_host_model_matches_reference_output_image(tmp_path, size, silver):
 
 
 def test_known_answers_present():
-    # force / try / silver screen / odd sizes / params variants
-    assert len(E2E) >= 9
+    # force / try / silver screen / odd sizes / params variants / full size
+    assert len(E2E) >= 10
+    assert "synth_1920x1080_s0_q95_force420" in E2E
     kinds = {k for e in E2E.values() for k in e["params"]}
     assert {"force_420", "try_420", "silver", "new_model", "lookahead"} <= kinds
 
@@ -72,7 +73,10 @@ def _params(gz, e):
 def test_process_420_known_answers(name):
     import guetzli_amd as gz
     e = E2E[name]
-    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    if e["input"].startswith("synthetic:"):
+        rgb = gz.synthetic_frame(int(e["input"].split(":")[1]), e["w"], e["h"])
+    else:
+        rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
     data, st = gz.process(rgb, e["w"], e["h"], _params(gz, e), return_stats=True)
     assert st.iterations == e["iters"]
     assert hashlib.sha256(data).hexdigest() == e["sha256"]
