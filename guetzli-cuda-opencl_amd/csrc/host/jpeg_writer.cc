@@ -818,6 +818,91 @@ bool WriteJpegSerial(const JpegData& jpg, bool strip_metadata, std::string* out)
   return true;
 }
 
+// WriteJpegSerial's output for any sampling layout (4:2:0 MCUs of 2x2 Y
+// blocks + Cb + Cr), the work split over MCU ranges on the host pool: the
+// histograms per range (each range's DC predictor is the component's last
+// block before it, so the differences are the serial pass's), then the scan
+// per range into raw bit buffers, concatenated and stuffed.
+bool WriteJpegParallel(const JpegData& jpg, bool strip_metadata, std::string* out) {
+  const int ncomps = static_cast<int>(jpg.components.size());
+  if (ncomps < 1 || ncomps > 4) return false;
+  const int mcus = jpg.mcu_rows * jpg.mcu_cols;
+  const int target = 4 * HostThreads();
+  const int per = std::max(64, (mcus + target - 1) / target);
+  const int chunks = (mcus + per - 1) / per;
+  bool grid = chunks > 1;
+  for (const JpegComponent& c : jpg.components)
+    grid = grid && c.width_in_blocks == jpg.mcu_cols * c.h_samp_factor &&
+           c.height_in_blocks == jpg.mcu_rows * c.v_samp_factor &&
+           c.coeffs.size() == static_cast<size_t>(c.width_in_blocks) * c.height_in_blocks * 64;
+  if (!grid) return WriteJpegSerial(jpg, strip_metadata, out);
+  auto block_of = [&](const JpegComponent& c, int m, int iy, int ix) {
+    const int my = m / jpg.mcu_cols, mx = m % jpg.mcu_cols;
+    return &c.coeffs[static_cast<size_t>((my * c.v_samp_factor + iy) * c.width_in_blocks +
+                                         mx * c.h_samp_factor + ix) << 6];
+  };
+  // the DC predictor of each component at the start of MCU m0
+  auto start_dc = [&](int ci, int m0) -> coeff_t {
+    if (m0 == 0) return 0;
+    const JpegComponent& c = jpg.components[ci];
+    return block_of(c, m0 - 1, c.v_samp_factor - 1, c.h_samp_factor - 1)[0];
+  };
+  if (!WriteHeaderSegments(jpg, strip_metadata, out)) return false;
+  std::vector<HuffTable> dc_tab(ncomps), ac_tab(ncomps);
+  {
+    std::vector<JpegHistogram> dc_c(static_cast<size_t>(chunks) * ncomps), ac_c(static_cast<size_t>(chunks) * ncomps);
+    ParallelFor(chunks, [&](int ch) {
+      const int m0 = ch * per, m1 = std::min(mcus, m0 + per);
+      for (int ci = 0; ci < ncomps; ++ci) {
+        const JpegComponent& c = jpg.components[ci];
+        JpegHistogram& dh = dc_c[static_cast<size_t>(ch) * ncomps + ci];
+        JpegHistogram& ah = ac_c[static_cast<size_t>(ch) * ncomps + ci];
+        coeff_t last = start_dc(ci, m0);
+        for (int m = m0; m < m1; ++m)
+          for (int iy = 0; iy < c.v_samp_factor; ++iy)
+            for (int ix = 0; ix < c.h_samp_factor; ++ix) {
+              const coeff_t* co = block_of(c, m, iy, ix);
+              dh.Add(Log2Floor(std::abs(co[0] - last)) + 1);
+              last = co[0];
+              UpdateACHistogramForBlock(co, &ah);
+            }
+      }
+    });
+    // (the MCU grid is every block of each component: BuildACHistograms'
+    // counts)
+    std::vector<JpegHistogram> dc_h(ncomps), ac_h(ncomps);
+    for (int ch = 0; ch < chunks; ++ch)
+      for (int ci = 0; ci < ncomps; ++ci) {
+        for (int k = 0; k + 1 < JpegHistogram::kSize; ++k) {
+          dc_h[ci].counts[k] += dc_c[static_cast<size_t>(ch) * ncomps + ci].counts[k];
+          ac_h[ci].counts[k] += ac_c[static_cast<size_t>(ch) * ncomps + ci].counts[k];
+        }
+      }
+    WriteHuffmanSegments(jpg, dc_h.data(), ac_h.data(), dc_tab.data(), ac_tab.data(), out);
+  }
+  std::vector<RawBits> parts(chunks);
+  ParallelFor(chunks, [&](int ch) {
+    const int m0 = ch * per, m1 = std::min(mcus, m0 + per);
+    RawBits& bw = parts[ch];
+    bw.Clear();
+    coeff_t last_dc[4];
+    for (int ci = 0; ci < ncomps; ++ci) last_dc[ci] = start_dc(ci, m0);
+    for (int m = m0; m < m1; ++m)
+      for (int ci = 0; ci < ncomps; ++ci) {
+        const JpegComponent& c = jpg.components[ci];
+        for (int iy = 0; iy < c.v_samp_factor; ++iy)
+          for (int ix = 0; ix < c.h_samp_factor; ++ix) {
+            const coeff_t* co = block_of(c, m, iy, ix);
+            EncodeBlock(bw, [co](int k) { return co[kJPEGNaturalOrder[k]]; }, &last_dc[ci], dc_tab[ci],
+                        ac_tab[ci]);
+          }
+      }
+  });
+  EmitStuffed(parts, chunks, out);
+  out->append("\xff\xd9", 2);
+  return true;
+}
+
 }  // namespace
 
 int StageCoeffImage(const CoeffImage& img, const JpegData& meta, ScanScratch* s) {
@@ -891,7 +976,7 @@ bool WriteCoeffImageJpeg(const CoeffImage& img, const JpegData& meta, bool strip
 
 bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
   // WriteJpeg (jpeg_data_writer.cc:540-553)
-  if (!IsOneBlockPerMcu(jpg)) return WriteJpegSerial(jpg, strip_metadata, out);
+  if (!IsOneBlockPerMcu(jpg)) return WriteJpegParallel(jpg, strip_metadata, out);
   ScanScratch s;
   const int ncomp = static_cast<int>(jpg.components.size());
   StageAll(jpg.mcu_cols * jpg.mcu_rows, ncomp, &s, [&](int c, int b, coeff_t* dst) {

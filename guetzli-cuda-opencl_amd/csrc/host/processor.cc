@@ -1586,8 +1586,9 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
         res_->seconds_backend += Since(tb);
         break;
       }
-      std::sort(global_order.begin(), global_order.end(),
-                [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; });
+      // std::sort(global_order) (processor.cc:825-828), materialised lazily:
+      // only the prefix the change loop consumes gets sorted (host/lazy_sort.h)
+      LazyStdSort sorter(global_order.data(), global_order.size());
       double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
       if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
       const double min_size_delta = base_size * rel_size_delta;
@@ -1595,15 +1596,18 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
       if (first_up_iter) {
         const float limit = 0.75f * cmp_->BlockErrorLimit();
-        const auto it = std::partition_point(global_order.begin(), global_order.end(),
-                                             [=](const std::pair<int, float>& a) { return a.second < limit; });
-        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, static_cast<int>(it - global_order.begin()));
+        // partition_point(key < limit) of the sorted order == count of keys below limit
+        int below = 0;
+        for (const auto& e : global_order) below += e.second < limit ? 1 : 0;
+        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, below);
         first_up_iter = false;
       }
       float val_threshold = 0.0f;
       int changed_coeffs = 0;
       int est_jpg_size = prev_size;
-      for (size_t i = 0; i < global_order.size(); ++i) {
+      const size_t n_order = global_order.size();
+      for (size_t i = 0; i < n_order; ++i) {
+        if (i >= sorter.sorted()) sorter.EnsureSorted(i);
         const int bix = global_order[i].first;
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
@@ -1624,7 +1628,14 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
         last_indexes[bix] += direction;
         val_threshold = global_order[i].second;
         ++changed_coeffs;
-        if (i % 10 == 0) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+        // the estimate is read only once changed_coeffs > min_coeffs_to_change
+        // and at the last step; a decade's codes only if such a step reads
+        // them (as the 4:4:4 back end) -- the same values where they are read
+        const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
+        if (i % 10 == 0 &&
+            (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs_to_change)) || i + 10 >= n_order))
+          ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+        if (!needed) continue;
         est_jpg_size = jpg_header_size + dc_size + ac_histogram_size +
                        static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
         if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta) break;
