@@ -434,7 +434,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4);
   alloc(reinterpret_cast<void**>(&e->d_zero_nnz_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_zero_bins_), 2 * kOrderBins * 4);
-  alloc(reinterpret_cast<void**>(&e->d_scan_sums_), (static_cast<size_t>(e->nb_) / kScanChunk + 1) * 4);
+  alloc(reinterpret_cast<void**>(&e->d_scan_sums_), (static_cast<size_t>(e->nb_) / 4 + 2) * 4);
   alloc(reinterpret_cast<void**>(&e->d_cand_idx_), static_cast<size_t>(e->nb_) * 192);
   alloc(reinterpret_cast<void**>(&e->d_cand_err_), static_cast<size_t>(e->nb_) * 192 * 4);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_zero_off_), static_cast<size_t>(e->nb_ + 1) * 4) != hipSuccess)
@@ -443,7 +443,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   alloc(reinterpret_cast<void**>(&e->d_jzz_), nc * sizeof(int16_t));
   alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
-  alloc(reinterpret_cast<void**>(&e->d_jhist_), 6 * 256 * 4 + 16);
+  alloc(reinterpret_cast<void**>(&e->d_jhist_), kJHistDeviceBytes);
   alloc(&e->d_jcodes_, sizeof(JpegCodesPacked));
   alloc(reinterpret_cast<void**>(&e->d_jbitlen_), static_cast<size_t>(e->nb_) * 4);
   alloc(reinterpret_cast<void**>(&e->d_jbitoff_), static_cast<size_t>(e->nb_ + 1) * 4);
@@ -458,7 +458,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodesPacked)) != hipSuccess)
     ok = false;
-  if (ok && (hipMemsetAsync(e->d_jhist_, 0, 6 * 256 * 4 + 16, s) != hipSuccess ||
+  if (ok && (hipMemsetAsync(e->d_jhist_, 0, kJHistDeviceBytes, s) != hipSuccess ||
              hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess))
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
@@ -1022,12 +1022,18 @@ static size_t BzLdsPad() {
 }
 
 // offsets[0..n] = exclusive prefix sums of the device counts[0..n), on the stream.
-bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name) {
+bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name,
+                        const int* group_sums, int per, uint32_t* zero_words, int* info) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (n > nb_) return Fail("ScanCounts size", 0);
   const unsigned chunks = static_cast<unsigned>((n + kScanChunk - 1) / kScanChunk);
-  GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
-                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets)));
+  if (group_sums) {
+    GZ_TIMED(name, k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, group_sums, per, offsets, zero_words, info));
+  } else {
+    GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
+                    k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, kScanChunk, offsets,
+                                                         zero_words, info)));
+  }
   return true;
 }
 
@@ -1230,12 +1236,11 @@ bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
   const JpegCodesPacked* dc = static_cast<const JpegCodesPacked*>(d_jcodes_);
   uint32_t* words = d_jwords_[jslot_];
   const unsigned mcu_groups = static_cast<unsigned>((nb_ + 3) / 4);
-  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_));
-  if (!ScanCounts(d_jbitlen_, nb_, d_jbitoff_, "jpeg_scan")) return false;
+  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_, d_scan_sums_));
+  if (!ScanCounts(d_jbitlen_, nb_, d_jbitoff_, "jpeg_scan", d_scan_sums_, 4, words, d_jinfo_)) return false;
   // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any scan)
-  GZ_TIMED("jpeg_emit", (k_zero_words<<<512, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_),
-                         k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
-                         k_jpeg_pad_count<<<256, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_,
+  GZ_TIMED("jpeg_emit", (k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
+                         k_jpeg_pad_count<<<64, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_,
                                                               m_jhist_ + 6 * 256 + 2)));
   // (0xff count, bit total) reach h_jhist_[1538..1539] from the last workgroup
   return true;

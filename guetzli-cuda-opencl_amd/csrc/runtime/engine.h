@@ -160,7 +160,9 @@ class Engine {
   bool Sync();
   void CompareFinish(float* distance, float* block_max);
   bool JpegScanFinish(uint64_t* nbits, uint64_t* ff);
-  bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
+  bool ScanCounts(const int* counts, int n, int* offsets, const char* name,
+                  const int* group_sums = nullptr, int per = 0, uint32_t* zero_words = nullptr,
+                  int* info = nullptr);
   bool OrderBlocks(int comp_mask);
 
   const std::string& error() const { return err_; }
@@ -230,13 +232,13 @@ class Engine {
   int* d_zero_off_ = nullptr;      // [blocks + 1] their offsets
   int* d_zero_nnz_ = nullptr;      // [blocks] non-zero AC counts (processing order)
   int* d_zero_bins_ = nullptr;     // [2][193] count histogram, scatter cursors
-  int* d_scan_sums_ = nullptr;     // [blocks / kScanChunk + 1] chunk totals
+  int* d_scan_sums_ = nullptr;     // [blocks / 4 + 2] chunk totals / 4-MCU group totals
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
   int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
   int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
   uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
-  uint32_t* d_jhist_ = nullptr;    //   6 x 256 counts + chroma non-zeros (u64) + done counter
+  uint32_t* d_jhist_ = nullptr;    //   kJHistCopies x 6 x 256 counts + chroma non-zeros (u64) + done counter
   void* d_jcodes_ = nullptr;       //   JpegCodesPacked
   int* d_jbitlen_ = nullptr;       //   [blocks]
   int* d_jbitoff_ = nullptr;       //   [blocks + 1]
