@@ -332,6 +332,8 @@ def main():
     ap.add_argument("--quality", type=int, default=95)
     ap.add_argument("--frames-per-step", type=int, default=8,
                     help="frames per GPU per step, encoded concurrently")
+    ap.add_argument("--in-flight", type=int, default=0,
+                    help="frames encoded at once per GPU (0: all frames of the step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-processes", type=int, default=8)
     ap.add_argument("--dist-selftest", action="store_true",
@@ -371,7 +373,8 @@ def main():
                for sd in row] for row in seeds]
     torch.cuda.synchronize()
 
-    pool = concurrent.futures.ThreadPoolExecutor(max_workers=args.frames_per_step)
+    in_flight = args.in_flight if args.in_flight > 0 else args.frames_per_step
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=in_flight)
 
     def encode(t):
         return gz.process_device(t.data_ptr(), w, h, params, device=dev, return_stats=True)
@@ -539,6 +542,7 @@ def main():
                                    args.frames_per_step, w, h, q),
                    "width": w, "height": h, "quality": q,
                    "frames_per_gpu_per_step": args.frames_per_step,
+                   "frames_in_flight": in_flight,
                    "parallelism": "image-sharded over %d GPU(s)%s" % (
                        world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
                    "search_iterations": iters},

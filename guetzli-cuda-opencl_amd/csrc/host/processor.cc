@@ -6,6 +6,8 @@
 #include "host/processor.h"
 
 #include <algorithm>
+#include <time.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -60,6 +62,12 @@ namespace {
 using Clock = std::chrono::steady_clock;
 inline double Since(Clock::time_point t0) {
   return std::chrono::duration<double>(Clock::now() - t0).count();
+}
+// CPU seconds of the calling thread (host-cost accounting in the detail map)
+inline double ThreadCpu() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
 }
 
 inline int Log2FloorNonZero(uint32_t n) { return 31 ^ __builtin_clz(n); }
@@ -321,6 +329,7 @@ bool HipButteraugliComparator::DeviceEncodeAndCompare(const CoeffImage& img,
   // builds the Huffman codes from the staged histograms while the Compare
   // pass runs, and waits once for both results.
   const auto t0 = Clock::now();
+  const double c0 = ThreadCpu();
   if (!SyncCoeffs(img)) return false;
   Engine* e = engine_.get();
   uint32_t hist[6 * 256];
@@ -349,6 +358,7 @@ bool HipButteraugliComparator::DeviceEncodeAndCompare(const CoeffImage& img,
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
   *size = cur_size_;
   seconds_compare += Since(t0);
+  cpu_compare += ThreadCpu() - c0;
   return true;
 }
 
@@ -1684,6 +1694,7 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
             int h, ProcessResult* result, std::string* err) {
   // guetzli::Process(params, stats, rgb, w, h, out), processor.cc:1157-1185
   const auto t0 = Clock::now();
+  const double c0 = ThreadCpu();
   if (w <= 0 || h <= 0 || w >= (1 << 16) || h >= (1 << 16)) {
     if (err) *err = "Could not create jpg data from rgb pixels";
     return GZ_ERR_INVALID_ARG;
@@ -1720,8 +1731,10 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
     result->compares = cmp->compares;
     result->seconds_compare = cmp->seconds_compare;
     result->seconds_zeroing = cmp->seconds_zeroing;
+    result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
   }
   result->seconds_total = Since(t0);
+  result->detail["thread_cpu_s"] = ThreadCpu() - c0;
   return rc;
 }
 
@@ -1729,6 +1742,7 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
                 ProcessResult* result, std::string* err) {
   // guetzli::Process(params, stats, data, jpg_out), processor.cc:1029-1066
   const auto t0 = Clock::now();
+  const double c0 = ThreadCpu();
   JpegData jpg;
   std::string rerr;
   if (!ReadJpeg(data, len, &jpg, &rerr)) {
@@ -1771,8 +1785,10 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     result->compares = cmp->compares;
     result->seconds_compare = cmp->seconds_compare;
     result->seconds_zeroing = cmp->seconds_zeroing;
+    result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
   }
   result->seconds_total = Since(t0);
+  result->detail["thread_cpu_s"] = ThreadCpu() - c0;
   return rc;
 }
 

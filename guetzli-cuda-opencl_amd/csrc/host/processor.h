@@ -184,6 +184,7 @@ class HipButteraugliComparator : public Comparator {
   bool OriginalJpegData(JpegData* jpg);
   Engine* engine() { return engine_.get(); }
   double seconds_compare = 0.0;
+  double cpu_compare = 0.0;  // calling thread's CPU seconds in the compares
   double seconds_zeroing = 0.0;
   int compares = 0;
 

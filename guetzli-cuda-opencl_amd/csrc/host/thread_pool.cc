@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <pthread.h>
+
 #include <condition_variable>
 #include <cstdlib>
 #include <list>
@@ -74,6 +76,7 @@ class Pool {
   void Work(Job* job) { Drain(job, job->next.fetch_add(1)); }
 
   void Loop() {
+    pthread_setname_np(pthread_self(), "gz_pool");  // per-thread CPU accounting
     for (;;) {
       Job* job = nullptr;
       int i;
