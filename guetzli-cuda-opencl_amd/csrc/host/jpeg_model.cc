@@ -128,6 +128,30 @@ void JpegHeaderFor(int w, int h, const int q[3][kDCTBlockSize], int ncomp, JpegD
   SaveQuantTables(q, jpg);
 }
 
+void JpegHeaderOf(const JpegData& jpg, JpegData* hdr) {
+  hdr->width = jpg.width;
+  hdr->height = jpg.height;
+  hdr->max_h_samp_factor = jpg.max_h_samp_factor;
+  hdr->max_v_samp_factor = jpg.max_v_samp_factor;
+  hdr->mcu_cols = jpg.mcu_cols;
+  hdr->mcu_rows = jpg.mcu_rows;
+  hdr->app_data = jpg.app_data;
+  hdr->com_data = jpg.com_data;
+  hdr->quant = jpg.quant;
+  hdr->components.resize(jpg.components.size());
+  for (size_t c = 0; c < jpg.components.size(); ++c) {
+    const JpegComponent& src = jpg.components[c];
+    JpegComponent& dst = hdr->components[c];
+    dst.id = src.id;
+    dst.h_samp_factor = src.h_samp_factor;
+    dst.v_samp_factor = src.v_samp_factor;
+    dst.quant_idx = src.quant_idx;
+    dst.width_in_blocks = src.width_in_blocks;
+    dst.height_in_blocks = src.height_in_blocks;
+    dst.coeffs.clear();
+  }
+}
+
 void CoeffImage::SaveHeaderToJpegData(int ncomp, JpegData* jpg) const {
   JpegHeaderFor(width, height, quant, ncomp, jpg);
 }

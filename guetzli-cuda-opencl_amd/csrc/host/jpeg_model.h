@@ -109,6 +109,9 @@ struct CoeffCursor {
 // The header part of SaveToJpegData for a w x h 4:4:4 image with quant q and
 // ncomp stored components (components without coefficients).
 void JpegHeaderFor(int w, int h, const int q[3][kDCTBlockSize], int ncomp, JpegData* jpg);
+// jpg's header fields (frame, components without coefficients, quant
+// tables, APPn / COM data) into *hdr.
+void JpegHeaderOf(const JpegData& jpg, JpegData* hdr);
 
 // Quantize (guetzli/quantize.h:25-30)
 inline coeff_t QuantizeCoeff(coeff_t raw, int quant) {

@@ -985,24 +985,7 @@ bool WriteJpeg(const JpegData& jpg, bool strip_metadata, std::string* out) {
     return 0;
   });
   s.ncomp = ncomp;
-  s.hdr.width = jpg.width;
-  s.hdr.height = jpg.height;
-  s.hdr.mcu_cols = jpg.mcu_cols;
-  s.hdr.mcu_rows = jpg.mcu_rows;
-  s.hdr.app_data = jpg.app_data;
-  s.hdr.com_data = jpg.com_data;
-  s.hdr.quant = jpg.quant;
-  s.hdr.components.resize(ncomp);
-  for (int c = 0; c < ncomp; ++c) {
-    const JpegComponent& src = jpg.components[c];
-    JpegComponent& dst = s.hdr.components[c];
-    dst.id = src.id;
-    dst.h_samp_factor = src.h_samp_factor;
-    dst.v_samp_factor = src.v_samp_factor;
-    dst.quant_idx = src.quant_idx;
-    dst.width_in_blocks = src.width_in_blocks;
-    dst.height_in_blocks = src.height_in_blocks;
-  }
+  JpegHeaderOf(jpg, &s.hdr);
   return EncodeStaged(&s, strip_metadata, out);
 }
 

@@ -229,13 +229,8 @@ int HistogramsFromStage(const uint32_t* hist, uint64_t chroma, JpegHistogram dc[
 
 // Headers (*prologue) and Huffman code tables of an image with these
 // histograms (WriteJpeg's table choice, jpeg_data_writer.cc).
-bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
-                 bool strip_metadata, int ncomp, JpegHistogram* dc_h, JpegHistogram* ac_h,
-                 std::string* prologue, JpegCodeTables* codes) {
-  JpegData hdr;
-  hdr.app_data = meta.app_data;
-  hdr.com_data = meta.com_data;
-  JpegHeaderFor(w, h, q, ncomp, &hdr);
+bool PrepareScanFor(const JpegData& hdr, bool strip_metadata, int ncomp, JpegHistogram* dc_h,
+                    JpegHistogram* ac_h, std::string* prologue, JpegCodeTables* codes) {
   HuffCodeTable dc_tab[3], ac_tab[3];
   prologue->clear();
   if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, prologue)) return false;
@@ -248,6 +243,16 @@ bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& me
       codes->ac_code[c][i] = static_cast<uint16_t>(ac_tab[c].code[i]);
     }
   return true;
+}
+
+bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                 bool strip_metadata, int ncomp, JpegHistogram* dc_h, JpegHistogram* ac_h,
+                 std::string* prologue, JpegCodeTables* codes) {
+  JpegData hdr;
+  hdr.app_data = meta.app_data;
+  hdr.com_data = meta.com_data;
+  JpegHeaderFor(w, h, q, ncomp, &hdr);
+  return PrepareScanFor(hdr, strip_metadata, ncomp, dc_h, ac_h, prologue, codes);
 }
 }  // namespace
 
@@ -325,6 +330,35 @@ bool HipButteraugliComparator::DeviceWriteJpeg(const CoeffImage& img, const Jpeg
 bool HipButteraugliComparator::DeviceEncodeAndCompare(const CoeffImage& img,
                                                       const JpegData& meta, bool strip_metadata,
                                                       size_t* size) {
+  return EncodeAndCompareWith(img, meta, nullptr, strip_metadata, size);
+}
+
+// The reference's first output, OutputJpeg(jpg_in) (processor.cc:965-967),
+// when jpg_in holds img's coefficients as they are (every quant value 1, as
+// for RGB input, one block per MCU): its scan is the device coder's scan of
+// img, only the headers are jpg_in's own (three quant tables where
+// SaveToJpegData shares one), so the size -- and, if it is kept, the bytes --
+// come from the device with jpg_in's prologue.  Not used (*used = false;
+// the Compare is done) when SaveToJpegData would drop all-zero chroma that
+// jpg_in keeps.
+bool HipButteraugliComparator::DeviceEncodeOriginalAndCompare(const CoeffImage& img,
+                                                              const JpegData& jpg_in,
+                                                              bool strip_metadata, size_t* size,
+                                                              bool* used) {
+  JpegData hdr;
+  JpegHeaderOf(jpg_in, &hdr);
+  *used = true;
+  if (!EncodeAndCompareWith(img, jpg_in, &hdr, strip_metadata, size)) {
+    if (err_ != "jpeg header components") return false;
+    err_.clear();
+    *used = false;
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const JpegData& meta,
+                                                    const JpegData* hdr, bool strip_metadata,
+                                                    size_t* size) {
   // One stream order: histogram stage, Compare pass, then the scan; the host
   // builds the Huffman codes from the staged histograms while the Compare
   // pass runs, and waits once for both results.
@@ -341,8 +375,22 @@ bool HipButteraugliComparator::DeviceEncodeAndCompare(const CoeffImage& img,
   JpegHistogram dc_h[3], ac_h[3];
   const int ncomp = HistogramsFromStage(hist, chroma, dc_h, ac_h);
   JpegCodeTables codes;
-  if (!PrepareScan(w_, h_, img.quant, meta, strip_metadata, ncomp, dc_h, ac_h, &cur_prologue_,
-                   &codes)) {
+  if (hdr && static_cast<int>(hdr->components.size()) != ncomp) {
+    // (the Compare is in the stream: finish it)
+    if (!e->Sync()) {
+      err_ = e->error();
+      return false;
+    }
+    e->CompareFinish(&distance_, block_max_.data());
+    ++compares;
+    seconds_compare += Since(t0);
+    cpu_compare += ThreadCpu() - c0;
+    err_ = "jpeg header components";
+    return false;
+  }
+  if (!(hdr ? PrepareScanFor(*hdr, strip_metadata, ncomp, dc_h, ac_h, &cur_prologue_, &codes)
+            : PrepareScan(w_, h_, img.quant, meta, strip_metadata, ncomp, dc_h, ac_h, &cur_prologue_,
+                          &codes))) {
     err_ = "jpeg header";
     return false;
   }
@@ -1354,8 +1402,14 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
     if (err) *err = "Unsupported sampling factors";
     return GZ_ERR_UNSUPPORTED;
   }
+  // The original's output (processor.cc:965-967) is written here on the
+  // host unless the device coder can give it (DeviceEncodeOriginalAndCompare)
   std::string encoded;
-  OutputJpeg(jpg_in, &encoded);
+  bool ones = true;
+  for (const QuantTable& t : jpg_in.quant)
+    for (int k = 0; k < kDCTBlockSize; ++k) ones = ones && t.values[k] == 1;
+  const bool orig_on_device = cmp_ && cmp_->HasDeviceWriter() && !input_is_420 && ones;
+  if (!orig_on_device) OutputJpeg(jpg_in, &encoded);
   final_score_ = -1;
   if (cmp_ == nullptr) {  // image too small for Butteraugli
     res_->jpeg = encoded;
@@ -1373,14 +1427,37 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
     if (!cmp_->SetOriginalCoeffs(jpg)) return device_error();
     img.Init(jpg.width, jpg.height);
     img.CopyFromJpegData(jpg);
-    if (!cmp_->Compare(img)) return device_error();
+    if (orig_on_device) {
+      size_t size = 0;
+      bool used = false;
+      if (!cmp_->DeviceEncodeOriginalAndCompare(img, jpg_in, params_.clear_metadata, &size, &used))
+        return device_error();
+      if (used) {
+        MaybeOutputDevice(size);  // the first output: always kept
+        if (getenv("GZ_CHECK_ORIGINAL_OUTPUT")) {  // test hook: bytes vs the host writer
+          std::string host, dev;
+          OutputJpeg(jpg_in, &host);
+          if (!cmp_->DeviceFetchKept(&dev)) return device_error();
+          if (host != dev || host.size() != size) {
+            if (err) *err = "device-coded original output differs from the host writer's";
+            return GZ_ERR_INTERNAL;
+          }
+        }
+      } else {
+        OutputJpeg(jpg_in, &encoded);
+        MaybeOutput(encoded);
+      }
+    } else {
+      if (!cmp_->Compare(img)) return device_error();
+      MaybeOutput(encoded);
+    }
   } else {
     Image420 im;
     im.Init(jpg.width, jpg.height);
     im.CopyFromJpegData(jpg);
     if (!cmp_->Compare420(im)) return device_error();
+    MaybeOutput(encoded);
   }
-  MaybeOutput(encoded);
   const int try_420 = (input_is_420 || params_.force_420 || (params_.try_420 && !IsGrayscale(jpg_in))) ? 1 : 0;
   const int force_420 = (input_is_420 || params_.force_420) ? 1 : 0;
   for (int downsample = force_420; downsample <= try_420; ++downsample) {

@@ -75,6 +75,14 @@ class Comparator {
                                       bool strip_metadata, size_t* size) {
     return DeviceEncode(img, meta, strip_metadata, size) && Compare(img);
   }
+  // Compare(img) and, when the comparator's device can code it, the size of
+  // WriteJpeg(jpg_in) for a jpg_in holding img's coefficients unquantized
+  // (its kept form via DeviceKeepEncoded); *used = false: write it on the host.
+  virtual bool DeviceEncodeOriginalAndCompare(const CoeffImage& img, const JpegData& jpg_in,
+                                              bool strip_metadata, size_t* size, bool* used) {
+    *used = false;
+    return Compare(img);
+  }
   virtual void DeviceKeepEncoded() {}
   virtual bool DeviceFetchKept(std::string* out) { return false; }
   // DC / AC histograms of img as SaveToJpegData stores it (comps at or above
@@ -159,6 +167,8 @@ class HipButteraugliComparator : public Comparator {
                     size_t* size) override;
   bool DeviceEncodeAndCompare(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                               size_t* size) override;
+  bool DeviceEncodeOriginalAndCompare(const CoeffImage& img, const JpegData& jpg_in,
+                                      bool strip_metadata, size_t* size, bool* used) override;
   void DeviceKeepEncoded() override;
   bool DeviceFetchKept(std::string* out) override;
   double seconds_encode = 0.0;  // host part of the overlapped encodes
@@ -190,6 +200,9 @@ class HipButteraugliComparator : public Comparator {
 
  private:
   bool SyncCoeffs(const CoeffImage& img);
+  // DeviceEncodeAndCompare with the headers of *hdr (nullptr: SaveToJpegData's)
+  bool EncodeAndCompareWith(const CoeffImage& img, const JpegData& meta, const JpegData* hdr,
+                            bool strip_metadata, size_t* size);
 
   std::unique_ptr<Engine> engine_;
   std::vector<coeff_t> orig_;      // q=1 coefficients of the original (host copy)

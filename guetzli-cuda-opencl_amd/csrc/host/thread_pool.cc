@@ -1,12 +1,15 @@
 #include "host/thread_pool.h"
 
+#include <pthread.h>
+#include <stdio.h>
+#include <time.h>
+
 #include <algorithm>
 #include <atomic>
-#include <pthread.h>
-
 #include <condition_variable>
 #include <cstdlib>
 #include <list>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -123,8 +126,58 @@ int HostThreads() {
   return n;
 }
 
-void ParallelFor(int n, const std::function<void(int)>& fn) {
+namespace {
+// GZ_POOL_PROFILE=1: CPU seconds of the items of every ParallelFor call
+// site (all threads), printed to stderr at exit -- where the host cores go.
+double ThreadCpuSeconds() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
+}
+struct SiteStats {
+  double cpu = 0.0;
+  long calls = 0, items = 0;
+};
+std::mutex g_prof_mu;
+std::map<std::pair<const char*, int>, SiteStats>* g_prof = nullptr;
+bool PoolProfiling() {
+  static const bool on = [] {
+    const char* e = std::getenv("GZ_POOL_PROFILE");
+    if (!(e && std::atoi(e) > 0)) return false;
+    g_prof = new std::map<std::pair<const char*, int>, SiteStats>();
+    std::atexit([] {
+      std::lock_guard<std::mutex> lk(g_prof_mu);
+      for (const auto& kv : *g_prof)
+        fprintf(stderr, "pool site %s:%d calls %ld items %ld cpu %.4f s\n", kv.first.first,
+                kv.first.second, kv.second.calls, kv.second.items, kv.second.cpu);
+    });
+    return true;
+  }();
+  return on;
+}
+}  // namespace
+
+void ParallelFor(int n, const std::function<void(int)>& fn, const char* file, int line) {
   if (n <= 0) return;
+  if (PoolProfiling()) {
+    std::atomic<long> ns{0};
+    const std::function<void(int)> timed = [&](int i) {
+      const double c0 = ThreadCpuSeconds();
+      fn(i);
+      ns += static_cast<long>(1e9 * (ThreadCpuSeconds() - c0));
+    };
+    if (n == 1 || HostThreads() == 1) {
+      for (int i = 0; i < n; ++i) timed(i);
+    } else {
+      GetPool()->Run(n, timed);
+    }
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    SiteStats& st = (*g_prof)[{file, line}];
+    st.cpu += 1e-9 * static_cast<double>(ns.load());
+    ++st.calls;
+    st.items += n;
+    return;
+  }
   if (n == 1 || HostThreads() == 1) {
     for (int i = 0; i < n; ++i) fn(i);
     return;

@@ -16,6 +16,8 @@ int HostThreads();
 // Runs fn(i) for i in [0, n) on the pool (the caller takes part) and returns
 // when all are done.  Items are handed out dynamically.  If another thread
 // is using the pool, the items run on the calling thread instead.
-void ParallelFor(int n, const std::function<void(int)>& fn);
+// (file / line: the call site, for GZ_POOL_PROFILE)
+void ParallelFor(int n, const std::function<void(int)>& fn, const char* file = __builtin_FILE(),
+                 int line = __builtin_LINE());
 
 }  // namespace gz

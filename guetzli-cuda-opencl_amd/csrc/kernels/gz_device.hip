@@ -1200,7 +1200,7 @@ bool Engine::JpegStageEnqueue(const int q[3][64]) {
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
   // (the device counts are zero: cleared at creation, and by the last
   // workgroup of every stage after it has published them to h_jhist_)
-  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * nb_ + 255) / 256, 256, 0, s>>>(
+  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * nb_ + kStageBlocks - 1) / kStageBlocks, 1024, 0, s>>>(
       d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;

@@ -337,3 +337,26 @@ def test_process_params_variants_known_answers(gz, name):
     data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
     assert st.iterations == e["iters"]
     assert hashlib.sha256(data).hexdigest() == e["sha256"]
+
+
+@pytest.mark.parametrize("kind", ["bees", "synthetic", "gray"])
+def test_device_coded_original_output_matches_host_writer(gz, kind, monkeypatch):
+    """The reference writes the original image first (processor.cc:965-967,
+    kept when no candidate scores better).  For RGB input the library codes
+    it on the device with the original's own headers; the hook compares
+    those bytes with the host writer's (the gray case, whose chroma
+    SaveToJpegData would drop, takes the host writer itself)."""
+    monkeypatch.setenv("GZ_CHECK_ORIGINAL_OUTPUT", "1")
+    if kind == "bees":
+        e = MANIFEST["e2e"]["bees_q90"]
+        rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+        w, h = e["w"], e["h"]
+    elif kind == "synthetic":
+        w, h = 333, 197
+        rgb = gz.synthetic_frame(11, w, h)
+    else:
+        w, h = 96, 64
+        g = gz.synthetic_frame(12, w, h).reshape(h, w, 3)[:, :, :1]
+        rgb = np.ascontiguousarray(np.repeat(g, 3, axis=2)).reshape(-1)
+    data = gz.process(rgb, w, h, gz.Params.for_quality(95))
+    assert data[:2] == b"\xff\xd8"
