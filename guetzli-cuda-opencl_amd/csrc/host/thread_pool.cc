@@ -8,6 +8,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <cstring>
 #include <list>
 #include <map>
 #include <mutex>
@@ -116,12 +117,35 @@ Pool* GetPool() {
 
 }  // namespace
 
+namespace {
+// CPUs this process may use: the affinity set, capped by a cgroup v2 CPU
+// quota (cpu.max "quota period"; a container's CPU share is often a quota,
+// not an affinity mask).
+int UsableCpus() {
+  int n = static_cast<int>(std::thread::hardware_concurrency());
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (fscanf(f, "%31s %ld", quota, &period) == 2 && period > 0 && std::strcmp(quota, "max") != 0) {
+      const long q = std::atol(quota);
+      if (q > 0) n = std::min<long>(n, std::max<long>(1, (q + period - 1) / period));
+    }
+    fclose(f);
+  }
+  return std::max(1, n);
+}
+}  // namespace
+
 int HostThreads() {
   static const int n = [] {
     const char* e = std::getenv("GZ_HOST_THREADS");
     if (e && std::atoi(e) > 0) return std::min(256, std::atoi(e));
-    const int hw = static_cast<int>(std::thread::hardware_concurrency());
-    return std::max(1, std::min(16, hw));
+    // the node's CPUs shared by the ranks on it (torch.distributed.run sets
+    // LOCAL_WORLD_SIZE), at most 16 per process
+    int share = UsableCpus();
+    const char* lw = std::getenv("LOCAL_WORLD_SIZE");
+    if (lw && std::atoi(lw) > 1) share /= std::atoi(lw);
+    return std::max(1, std::min(16, share));
   }();
   return n;
 }

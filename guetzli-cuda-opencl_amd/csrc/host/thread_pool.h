@@ -1,7 +1,8 @@
 // Fixed-size host worker pool for the data-parallel host passes of the search
 // loop (scan encoding, histograms).  One pool per process.  The worker count
-// is GZ_HOST_THREADS, else min(16, hardware threads) — 16 being the CPU share
-// a GPU gets on the target nodes.  The pool is not re-entrant; callers that
+// is GZ_HOST_THREADS, else min(16, the usable CPUs -- affinity and cgroup
+// quota -- divided by LOCAL_WORLD_SIZE ranks) -- 16 being the CPU share a
+// GPU gets on the target nodes.  The pool is not re-entrant; callers that
 // find it busy run their items inline (ParallelFor).
 #pragma once
 
