@@ -763,8 +763,11 @@ size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::ve
 // before rounding -- for the current depths.
 struct AcBlockModel {
   std::vector<uint64_t> nz;  // [c * blocks + b]: bit z set <=> zigzag coefficient z non-zero
+  float inv_q[3][kDCTBlockSize];  // 1 / quant (natural order), for Size
 
   void Build(const CoeffImage& img) {
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < kDCTBlockSize; ++k) inv_q[c][k] = 1.0f / static_cast<float>(img.quant[c][k]);
     nz.assign(static_cast<size_t>(3) * img.blocks, 0);
     for (int c = 0; c < 3; ++c)
       for (int b = 0; b < img.blocks; ++b) {
@@ -776,6 +779,15 @@ struct AcBlockModel {
   }
 
   static int Size(coeff_t v, int q) { return Log2FloorNonZero(std::abs(v / q)) + 1; }
+  // Size(v, q) without the integer division: |v| / q rounded through the
+  // float reciprocal is within one of the quotient (|v| < 2^16, relative
+  // error < 2^-22), and one multiply-compare settles it on the truncated one.
+  static int SizeInv(coeff_t v, int q, float inv) {
+    const int a = std::abs(static_cast<int>(v));
+    int n = static_cast<int>(static_cast<float>(a) * inv + 0.5f);
+    if (n * q > a) --n;
+    return Log2FloorNonZero(static_cast<uint32_t>(n)) + 1;
+  }
 
   // weight * symbols of the segment after non-zero position p (0 = none /
   // DC) through the non-zeros `mid` (0: none) and `nx` (0: none; then EOB
@@ -818,9 +830,11 @@ struct AcBlockModel {
     const uint64_t above = z < 63 ? m & ~((2ull << z) - 1) : 0;
     const int p = below ? 63 - __builtin_clzll(below) : 0;
     const int nx = above ? __builtin_ctzll(above) : 0;
-    const int nx_size = nx ? Size(block[kJPEGNaturalOrder[nx]], q[kJPEGNaturalOrder[nx]]) : 0;
-    Segment(-1, p, old ? z : 0, old ? Size(old, q[k]) : 0, nx, nx_size, depth, h, raw);
-    Segment(1, p, newval ? z : 0, newval ? Size(newval, q[k]) : 0, nx, nx_size, depth, h, raw);
+    const int knx = kJPEGNaturalOrder[nx];
+    const int nx_size = nx ? SizeInv(block[knx], q[knx], inv_q[c][knx]) : 0;
+    Segment(-1, p, old ? z : 0, old ? SizeInv(old, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h, raw);
+    Segment(1, p, newval ? z : 0, newval ? SizeInv(newval, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h,
+            raw);
     if (newval) m |= 1ull << z; else m &= ~(1ull << z);
   }
 };
