@@ -579,51 +579,74 @@ void BlockErrorAdjustmentWeights(int w, int h, float target, int direction, int 
   const int sizex = 8 * factor_x, sizey = 8 * factor_y;
   const int bw = (w + sizex - 1) / sizex, bh = (h + sizey - 1) / sizey;
   const int r = max_block_dist;
-  auto max_local = [&](int bx, int by) {
-    float m = static_cast<float>(target_distance);
-    const int x0 = std::max(0, bx - r), y0 = std::max(0, by - r);
-    const int x1 = std::min(bw, bx + 1 + r), y1 = std::min(bh, by + 1 + r);
-    for (int y = y0; y < y1; ++y)
-      for (int x = x0; x < x1; ++x) m = std::max(m, max_dist_per_block[y * bw + x]);
-    return m;
-  };
   constexpr int kRows = 8;
   const int chunks = (bh + kRows - 1) / kRows;
+  const size_t nblk = static_cast<size_t>(bw) * bh;
+  // max_local(bx, by) = max(target, block maxima within Chebyshev radius r),
+  // separably: the row maxima over [bx - r, bx + r], then their maximum over
+  // [by - r, by + r] (a max of the same values: exact)
+  std::vector<float> rowmax(nblk), local(nblk);
+  ParallelFor(chunks, [&](int ch) {
+    for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        float m = static_cast<float>(target_distance);
+        for (int x = std::max(0, bx - r); x < std::min(bw, bx + 1 + r); ++x)
+          m = std::max(m, max_dist_per_block[by * bw + x]);
+        rowmax[by * bw + bx] = m;
+      }
+  });
+  ParallelFor(chunks, [&](int ch) {
+    for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        float m = static_cast<float>(target_distance);
+        for (int y = std::max(0, by - r); y < std::min(bh, by + 1 + r); ++y) m = std::max(m, rowmax[y * bw + bx]);
+        local[by * bw + bx] = m;
+      }
+  });
   if (direction > 0) {
     ParallelFor(chunks, [&](int ch) {
       for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
         for (int bx = 0; bx < bw; ++bx) {
           const int bix = by * bw + bx;
-          if (max_dist_per_block[bix] <= target_distance && max_local(bx, by) <= 1.1 * target_distance)
+          if (max_dist_per_block[bix] <= target_distance && local[bix] <= 1.1 * target_distance)
             (*block_weight)[bix] = 1.0;
         }
     });
     return;
   }
   constexpr double kLocalMaxWeight = 0.5;
-  std::vector<uint8_t> active(static_cast<size_t>(bw) * bh);
+  std::vector<uint8_t> active(nblk);
   ParallelFor(chunks, [&](int ch) {
     for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
       for (int bx = 0; bx < bw; ++bx) {
         const int bix = by * bw + bx;
         active[bix] = !(max_dist_per_block[bix] <=
-                        (1 - kLocalMaxWeight) * target_distance + kLocalMaxWeight * max_local(bx, by));
+                        (1 - kLocalMaxWeight) * target_distance + kLocalMaxWeight * local[bix]);
+      }
+  });
+  // every active block within Chebyshev distance d <= r raises the weight to
+  // 1 / (d + 1): the largest such term is the nearest active block's, found
+  // separably (nearest active in the row, then min over rows of
+  // max(|dy|, that)); the weight is the max of the same float terms as the
+  // per-neighbour loop
+  std::vector<int> hx(nblk);
+  ParallelFor(chunks, [&](int ch) {
+    for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        int d = r + 1;
+        for (int x = std::max(0, bx - r); x < std::min(bw, bx + 1 + r); ++x)
+          if (active[by * bw + x]) d = std::min(d, std::abs(x - bx));
+        hx[by * bw + bx] = d;
       }
   });
   ParallelFor(chunks, [&](int ch) {
     for (int by = ch * kRows; by < std::min(bh, (ch + 1) * kRows); ++by)
       for (int bx = 0; bx < bw; ++bx) {
         const int ix = by * bw + bx;
-        float wgt = (*block_weight)[ix];
-        const int x0 = std::max(0, bx - r), y0 = std::max(0, by - r);
-        const int x1 = std::min(bw, bx + 1 + r), y1 = std::min(bh, by + 1 + r);
-        for (int y = y0; y < y1; ++y)
-          for (int x = x0; x < x1; ++x) {
-            if (!active[y * bw + x]) continue;
-            const int d = std::max(std::abs(y - by), std::abs(x - bx));
-            wgt = std::max<float>(wgt, 1.0f / (d + 1.0f));
-          }
-        (*block_weight)[ix] = wgt;
+        int d = r + 1;
+        for (int y = std::max(0, by - r); y < std::min(bh, by + 1 + r); ++y)
+          d = std::min(d, std::max(std::abs(y - by), hx[y * bw + bx]));
+        if (d <= r) (*block_weight)[ix] = std::max<float>((*block_weight)[ix], 1.0f / (d + 1.0f));
       }
   });
 }
