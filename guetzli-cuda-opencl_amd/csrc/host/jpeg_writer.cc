@@ -158,7 +158,57 @@ int JpegHistogram::NumSymbols() const {
   return n;
 }
 
+namespace {
+void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth, uint8_t* depth);
+
+// The back end rebuilds its entropy codes every 10 coefficient changes; most
+// rebuilds leave some component histograms (and their merged pair) as they
+// were, so the last few results are kept per thread and reused when the
+// counts are identical (checked in full; the function is pure).
+struct CodeLengthCache {
+  static constexpr int kSlots = 8;
+  struct Slot {
+    uint64_t hash = 0;
+    int length = -1, max_depth = 0;
+    uint32_t counts[JpegHistogram::kSize];
+    uint8_t depth[JpegHistogram::kSize];
+  };
+  Slot slot[kSlots];
+  int next = 0;
+};
+}  // namespace
+
 void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t* depth) {
+  if (length > JpegHistogram::kSize) {
+    HuffmanCodeLengthsUncached(data, length, max_depth, depth);
+    return;
+  }
+  static thread_local CodeLengthCache cache;
+  uint64_t hsh = 1469598103934665603ull;
+  for (int i = 0; i < length; ++i) hsh = (hsh ^ data[i]) * 1099511628211ull;
+  for (CodeLengthCache::Slot& e : cache.slot)
+    if (e.hash == hsh && e.length == length && e.max_depth == max_depth &&
+        std::memcmp(e.counts, data, length * sizeof(uint32_t)) == 0) {
+      // (depth[] of the symbols the tree does not cover is left as the
+      // caller set it, as the uncached call does)
+      for (int i = 0; i < length; ++i)
+        if (data[i]) depth[i] = e.depth[i];
+      return;
+    }
+  CodeLengthCache::Slot& e = cache.slot[cache.next];
+  cache.next = (cache.next + 1) % CodeLengthCache::kSlots;
+  std::memset(e.depth, 0, sizeof(e.depth));
+  HuffmanCodeLengthsUncached(data, length, max_depth, e.depth);
+  e.hash = hsh;
+  e.length = length;
+  e.max_depth = max_depth;
+  std::memcpy(e.counts, data, length * sizeof(uint32_t));
+  for (int i = 0; i < length; ++i)
+    if (data[i]) depth[i] = e.depth[i];
+}
+
+namespace {
+void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth, uint8_t* depth) {
   // Huffman tree with iterative count flattening until it fits max_depth
   // (CreateHuffmanTree, entropy_encode.cc:65-145).  Leaves sorted by
   // (count asc, symbol desc): a total order, so any correct sort agrees --
@@ -211,6 +261,8 @@ void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t
     if (height[2 * n - 1] <= max_depth && AssignDepths(2 * n - 1, tree, depth, max_depth)) break;
   }
 }
+
+}  // namespace
 
 size_t HistogramHeaderCost(const JpegHistogram& h) {
   size_t bits = 17 * 8;
