@@ -53,13 +53,6 @@ const double kBlockCsfD[37] = {
     0.3831134973, 0.36198671102, 1.05178802919, 0.3831134973, 0.12,
 };
 
-const int kIdct[64] = {
-    8192, 11363, 10703, 9633,   8192,  6437,   4433,   2260,   8192, 9633,  4433,  -2259, -8192,
-    -11362, -10704, -6436, 8192, 6437, -4433,  -11362, -8192, 2261,   10704,  9633, 8192,  2260,
-    -10703, -6436, 8192, 9633,  -4433, -11363, 8192,   -2260, -10703, 6436,   8192, -9633, -4433,
-    11363,  8192,  -6437, -4433, 11362, -8192, -2261,  10704, -9633,  8192,   -9633, 4433, 2259,
-    -8192,  11362, -10704, 6436, 8192,  -11363, 10703, -9633, 8192,   -6437,  4433,  -2260,
-};
 
 // (extmul, extoff, offset, scaler, mul) of MaskX..MaskDcB, clbutter_comparator.cpp:994-1064
 const float kMaskParams[6][5] = {
@@ -148,7 +141,7 @@ void BuildTables(GzTables* t) {
     memcpy(t->zigzag, kZigZag, sizeof(kZigZag));
     memcpy(t->old_csf, kOldCsf, sizeof(kOldCsf));
   }
-  memcpy(t->idct, kIdct, sizeof(kIdct));
+  memcpy(t->idct, kIdctM, sizeof(kIdctM));
   BuildBlur(1.1f, 0.0f, &t->blur[kSigOpsin]);
   BuildBlur(1.5f, 0.0f, &t->blur[kSigEdgeX]);
   BuildBlur(0.586f, 0.0f, &t->blur[kSigEdgeY]);
@@ -724,7 +717,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   if (cand_src_ == kCandRgb) {
     GZ_TIMED("rgb_to_linear", k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_cand_rgb_, n_, d_lin_));
   } else {
-    GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(
+    GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + kC2lBlocks - 1) / kC2lBlocks, bh_), 256, 0, s>>>(
         d_cur_, w_, h_, bw_, nb_, d_lin_, cand_src_ == kCand420 ? d_planes_ : nullptr));
   }
   if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
