@@ -214,28 +214,30 @@ __device__ __forceinline__ double interp_d(const double* a, int size, double sx)
 // XybLowFreqToValsOpt + XybDiffLowFreqSquaredAccumulateOpt with the second
 // colour == 0 (the only form used on the path), :253-299.
 __device__ __forceinline__ void lowfreq_sq_zero_f(float x, float y, float z, float factor,
-                                                  float res[3]) {
+                                                  float res[3], const float* lf_dy = c_tab.lf_dy) {
   z += 0.0812519812628f * y;
   const float vz = z * 7.34905756986f;
   const float vx = x * 6.64482198135f;
-  const float vy = interp_f(c_tab.lf_dy, 21, y * 0.837846224276f);
+  const float vy = interp_f(lf_dy, 21, y * 0.837846224276f);
   res[0] += factor * vx * vx;
   res[1] += factor * vy * vy;
   res[2] += factor * vz * vz;
 }
 
-__device__ __forceinline__ void lowfreq_vals_f(float x, float y, float z, float v[3]) {
+// (lf_dy: c_tab.lf_dy or an LDS copy of it)
+__device__ __forceinline__ void lowfreq_vals_f(float x, float y, float z, float v[3],
+                                               const float* lf_dy = c_tab.lf_dy) {
   z += 0.0812519812628f * y;
   v[2] = z * 7.34905756986f;
   v[0] = x * 6.64482198135f;
-  v[1] = interp_f(c_tab.lf_dy, 21, y * 0.837846224276f);
+  v[1] = interp_f(lf_dy, 21, y * 0.837846224276f);
 }
 
 // General two-colour form (used by the corner edge detector).
 __device__ __forceinline__ void lowfreq_sq_f(const float a[3], const float b[3], float factor,
-                                             float res[3]) {
+                                             float res[3], const float* lf_dy = c_tab.lf_dy) {
   float v0[3];
-  lowfreq_vals_f(a[0], a[1], a[2], v0);
+  lowfreq_vals_f(a[0], a[1], a[2], v0, lf_dy);
   if (b[0] == 0.0f && b[1] == 0.0f && b[2] == 0.0f) {
     res[0] += factor * v0[0] * v0[0];
     res[1] += factor * v0[1] * v0[1];
@@ -243,7 +245,7 @@ __device__ __forceinline__ void lowfreq_sq_f(const float a[3], const float b[3],
     return;
   }
   float v1[3];
-  lowfreq_vals_f(b[0], b[1], b[2], v1);
+  lowfreq_vals_f(b[0], b[1], b[2], v1, lf_dy);
   const float dx = v0[0] - v1[0], dy = v0[1] - v1[1], dz = v0[2] - v1[2];
   res[0] += factor * dx * dx;
   res[1] += factor * dy * dy;
