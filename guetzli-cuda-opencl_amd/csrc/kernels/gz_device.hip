@@ -988,7 +988,7 @@ static long long* BzTraceBuf(int nb, void* stream) {
   if (nb > cap) {
     if (buf) hipFree(buf);
     buf = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&buf), static_cast<size_t>(nb) * 24) != hipSuccess) return nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), static_cast<size_t>(nb) * 32) != hipSuccess) return nullptr;
     cap = nb;
   }
   (void)stream;
@@ -997,7 +997,7 @@ static long long* BzTraceBuf(int nb, void* stream) {
 static void BzTraceDump(long long* buf, int nb, void* stream) {
   static const char* path = getenv("GZ_BZ_TRACE");
   if (!buf || !path) return;
-  std::vector<long long> h(static_cast<size_t>(nb) * 3);
+  std::vector<long long> h(static_cast<size_t>(nb) * 4);  // (start, end, steps, list sorted)
   if (hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)) != hipSuccess ||
       hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess)
     return;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Timeline of one k_block_zeroing launch: encodes a synthetic frame with
 GZ_BZ_TRACE set (the engine records each block's start / end on the 100 MHz
-wall clock and its greedy step count) and reports the span, the per-block
+wall clock, its greedy step count and when its candidate list was sorted) and reports the span, the per-block
 duration distribution, how much of the span the longest blocks alone take
 (the launch's critical path) and how many blocks are in flight over time.
 
@@ -27,8 +27,9 @@ def main():
             "rgb = gz.synthetic_frame(0, %d, %d); gz.process(rgb, %d, %d, gz.Params.for_quality(%d))"
             % (os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"), w, h, w, h, q))
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
-    t = np.fromfile(path, dtype=np.int64).reshape(-1, 3)
-    start, end, steps = t[:, 0], t[:, 1], t[:, 2]
+    t = np.fromfile(path, dtype=np.int64).reshape(-1, 4)
+    start, end, steps, sorted_t = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+    setup = (sorted_t - start) / 100.0  # us: reference opsin, IDCT, candidate keys + sort
     t0 = start.min()
     dur = (end - start) / 100.0  # us
     span = (end.max() - t0) / 100.0
@@ -43,6 +44,8 @@ def main():
         "span_us": round(span, 1),
         "block_us": {"mean": round(float(dur.mean()), 2), "median": round(float(np.median(dur)), 2),
                      "p99": round(float(np.percentile(dur, 99)), 1), "max": round(float(dur.max()), 1)},
+        "setup_us": {"mean": round(float(setup.mean()), 2), "median": round(float(np.median(setup)), 2),
+                     "p99": round(float(np.percentile(setup, 99)), 1), "sum": round(float(setup.sum()), 0)},
         "steps": {"mean": round(float(steps.mean()), 2), "max": int(steps.max()),
                   "total": int(steps.sum())},
         "us_per_step": {"median": round(float(np.median(per_step[steps > 0])), 3),
