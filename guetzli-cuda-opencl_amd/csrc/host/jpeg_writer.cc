@@ -221,7 +221,7 @@ void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth,
   // reference's loop, so the same depths.
   TreeNode tree[2 * JpegHistogram::kSize + 2];
   uint8_t height[2 * JpegHistogram::kSize + 2];
-  uint64_t base[JpegHistogram::kSize], keys[JpegHistogram::kSize];
+  uint64_t base[JpegHistogram::kSize], bysym[JpegHistogram::kSize], keys[JpegHistogram::kSize];
   int n = 0;
   for (int i = length - 1; i >= 0; --i)
     if (data[i]) base[n++] = (static_cast<uint64_t>(data[i]) << 16) | (0xffff - i);
@@ -230,13 +230,16 @@ void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth,
     depth[0xffff - (base[0] & 0xffff)] = 1;
     return;
   }
+  std::copy(base, base + n, bysym);  // (filled by descending symbol)
   std::sort(base, base + n);
   for (uint32_t count_limit = 1;; count_limit *= 2) {
-    // leaves with count <= count_limit: key (count_limit, symbol)
+    // leaves with count <= count_limit: key (count_limit, symbol), i.e.
+    // ordered by descending symbol -- bysym's order, filtered (no sort)
     int low = 0;
     while (low < n && (base[low] >> 16) <= count_limit) ++low;
-    for (int k = 0; k < low; ++k) keys[k] = (static_cast<uint64_t>(count_limit) << 16) | (base[k] & 0xffff);
-    std::sort(keys, keys + low);
+    int m = 0;
+    for (int k = 0; k < n && m < low; ++k)
+      if ((bysym[k] >> 16) <= count_limit) keys[m++] = (static_cast<uint64_t>(count_limit) << 16) | (bysym[k] & 0xffff);
     std::copy(base + low, base + n, keys + low);
     for (int k = 0; k < n; ++k) {
       tree[k] = TreeNode{static_cast<uint32_t>(keys[k] >> 16), -1,
