@@ -208,6 +208,70 @@ void HuffmanCodeLengths(const uint32_t* data, int length, int max_depth, uint8_t
 }
 
 namespace {
+// Sorts the n leaf keys (count << 16 | 0xffff - symbol: distinct, so the
+// sorted order is unique).  The back end asks for the codes of slowly
+// changing histograms, so the last few sorted symbol orders are kept per
+// thread; when one of them, re-keyed with the new counts, is nearly sorted
+// it is finished by insertion sort (linear plus the few inversions),
+// otherwise std::sort.
+void SortLeaves(uint64_t* keys, int n, const uint32_t* data, int length) {
+  struct Orders {
+    int n[2] = {0, 0};
+    uint16_t sym[2][JpegHistogram::kSize];
+    int next = 0;
+  };
+  static thread_local Orders cache;
+  uint64_t seq[JpegHistogram::kSize];
+  int best = -1, best_desc = n / 8 + 1;
+  if (length <= JpegHistogram::kSize) {
+    for (int o = 0; o < 2; ++o) {
+      if (cache.n[o] < 2) continue;
+      int m = 0, desc = 0;
+      uint64_t prev = 0;
+      for (int k = 0; k < cache.n[o]; ++k) {
+        const int sy = cache.sym[o][k];
+        if (sy >= length || !data[sy]) continue;
+        const uint64_t key = (static_cast<uint64_t>(data[sy]) << 16) | (0xffff - sy);
+        desc += m > 0 && prev > key ? 1 : 0;
+        prev = key;
+        ++m;
+      }
+      desc += n - m;  // leaves the order lacks (appended below)
+      if (desc < best_desc) {
+        best_desc = desc;
+        best = o;
+      }
+    }
+  }
+  if (best < 0) {
+    std::sort(keys, keys + n);
+  } else {
+    bool in[JpegHistogram::kSize] = {false};
+    int m = 0;
+    for (int k = 0; k < cache.n[best]; ++k) {
+      const int sy = cache.sym[best][k];
+      if (sy >= length || !data[sy]) continue;
+      seq[m++] = (static_cast<uint64_t>(data[sy]) << 16) | (0xffff - sy);
+      in[sy] = true;
+    }
+    for (int k = 0; k < n; ++k)
+      if (!in[0xffff - (keys[k] & 0xffff)]) seq[m++] = keys[k];
+    for (int i = 1; i < m; ++i) {  // insertion sort
+      const uint64_t v = seq[i];
+      int j = i;
+      for (; j > 0 && seq[j - 1] > v; --j) seq[j] = seq[j - 1];
+      seq[j] = v;
+    }
+    std::copy(seq, seq + n, keys);
+  }
+  if (length <= JpegHistogram::kSize) {
+    Orders& c = cache;
+    c.n[c.next] = n;
+    for (int k = 0; k < n; ++k) c.sym[c.next][k] = static_cast<uint16_t>(0xffff - (keys[k] & 0xffff));
+    c.next ^= 1;
+  }
+}
+
 void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth, uint8_t* depth) {
   // Huffman tree with iterative count flattening until it fits max_depth
   // (CreateHuffmanTree, entropy_encode.cc:65-145).  Leaves sorted by
@@ -231,7 +295,7 @@ void HuffmanCodeLengthsUncached(const uint32_t* data, int length, int max_depth,
     return;
   }
   std::copy(base, base + n, bysym);  // (filled by descending symbol)
-  std::sort(base, base + n);
+  SortLeaves(base, n, data, length);
   for (uint32_t count_limit = 1;; count_limit *= 2) {
     // leaves with count <= count_limit: key (count_limit, symbol), i.e.
     // ordered by descending symbol -- bysym's order, filtered (no sort)
