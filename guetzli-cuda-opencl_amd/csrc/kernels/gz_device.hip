@@ -759,6 +759,9 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // combined value; the search's passes apply the mask LUTs per sample in
   // the vertical pass and combine without them)
   const bool full_mask = dbg && (dbg->mask || dbg->mask_dc || dbg->combined);
+  // EdgeDetectorLowFreq's term is fused into k_combine_channels unless a
+  // stage dump wants the AC values with it, or k_combine runs
+  const bool fuse_lf = !full_mask && !(dbg && dbg->block_ac_lf);
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -788,7 +791,9 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     }
     const dim3 gv = BlurVStreamGrid(w_, h_, 9, bp);  // fills bp's packed-grid fields
     GZ_TIMED("blur_v", k_blur_vstream<kBlurLfMask><<<gv, 256, 0, s>>>(bp, w_, h_, d_scales_, scale_stride_));
-    GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
+    // (the search's passes add the low-frequency term in k_combine_channels)
+    if (!fuse_lf)
+      GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
   if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
   MaskPlanes mk = MaskPlanesOf(d_ma_, n, !full_mask);
@@ -806,8 +811,11 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
   } else {
     const MaskPlanes mkdc = MaskPlanesOf(d_mb_, n, true);
+    const size_t ldn = static_cast<size_t>((w_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]) *
+                       ((h_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]);
     GZ_TIMED("combine_channels", k_combine_channels<<<PixGrid(rw_, rh_), 256, 0, s>>>(
-        mk, mkdc, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_, d_resval_));
+        mk, mkdc, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_, d_resval_, fuse_lf ? d_bl_ : nullptr,
+        fuse_lf ? d_bl_ + 3 * ldn : nullptr));
   }
   // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
   {
