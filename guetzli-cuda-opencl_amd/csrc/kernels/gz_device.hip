@@ -744,11 +744,16 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     GZ_TIMED("edge_mask", k_edge_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(
         d_m0_, d_m1_, w_, h_, strips, segs, rows, d_bl_, d_mb_, d_scales_, scale_stride_));
   }
-  GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
+  // (the search's passes compute the edge term in k_block_diff; the stage
+  // dumps keep k_edge_map, whose output they read before block_diff runs)
+  const bool fuse_edge = !(dbg && dbg->edge);
+  if (!fuse_edge)
+    GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
   GZ_TIMED("block_diff", k_block_diff<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), 256, 0, s>>>(
-      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_));
+      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_, fuse_edge ? d_bl_ : nullptr,
+      fuse_edge ? d_bl_ + 3 * n : nullptr, d_edge_));
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
   // S7 + S12: the six sigma-14 blurs (low-frequency edge term, m0 / m1) and
