@@ -65,11 +65,12 @@ def stage_bytes_per_px():
     s["opsin_mhic"] = 3 * 4 + 3 * 4 + 6 * 4          # S1-S3 fused: linear + ref XYB -> m0, m1
     s["edge_blur"] = 6 * 4 + 6 * 4                  # S4: 6 separable blurs, 6 -> 6
     s["edge_mask"] = 6 * 4 + 6 * 4 + 3 * 4          # S4 + S9-S11 fused: 6 -> 6 blurred + 3 mask front
-    s["edge_map"] = 6 * 4 + 3 * 4 / 9.0
-    s["block_diff"] = 6 * 4 + 6 * 4 / 9.0
+    s["edge_map"] = 6 * 4 + 3 * 4 / 9.0              # (stage dumps only; fused into block_diff)
+    # S6 + S5 fused: m0 / m1 and the edge-blurred planes -> dc, ac, edge
+    s["block_diff"] = 6 * 4 + 6 * 4 + 9 * 4 / 9.0
     s["lowfreq_blur_h"] = 6 * 4 + 6 * 4 / 4.0
     s["lowfreq_blur_v"] = 6 * 4 / 4.0 + 6 * 4 / 16.0
-    s["low_freq"] = 6 * 4 / 16.0 + 2 * 3 * 4 / 9.0
+    s["low_freq"] = 6 * 4 / 16.0 + 2 * 3 * 4 / 9.0   # (stage dumps only; fused into combine_channels)
     s["mask_front"] = 6 * 4 + 3 * 4                 # S9-S11 fused: 6 planes -> 3
     s["mask_blur_h"] = 3 * 4 + 4 * (1 / 3.0 + 1 / 4.0 + 1.0)
     s["mask_blur_v"] = 4 * (1 / 3.0 + 1 / 4.0 + 1.0) + 4 * (1 / 9.0 + 1 / 16.0 + 1.0)
@@ -78,7 +79,9 @@ def stage_bytes_per_px():
     # blurred mask sample: one more decimated plane per channel)
     s["blur_v"] = s["lowfreq_blur_v"] + s["mask_blur_v"] + 4 * (1 / 9.0 + 1 / 16.0 + 1 / 9.0)
     s["combine"] = (3 * 4 + 3 * 4 + 3 * 4 + 3 * 4 + 4) / 9.0
-    s["combine_channels"] = (6 * 4 + 9 * 4 + 4) / 9.0    # S14/S15: LUT'd mask samples + dc/ac/edge -> R
+    # S14/S15 + S8 fused: LUT'd mask samples + dc/ac/edge -> R, and the
+    # sigma-14 planes (1/16 density) for the low-frequency term
+    s["combine_channels"] = (6 * 4 + 9 * 4 + 4) / 9.0 + 6 * 4 / 16.0
     s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
     s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
     s["diffmap_final"] = 4 / 9.0 + 4 / 4.0 + 4 / 64.0
@@ -90,6 +93,12 @@ def stage_bytes_per_px():
 # (192 B) and its 3 mask scales; writes its 192-entry CoeffData order (8 B
 # each) and its kept-entry count.
 ZEROING_BYTES_PER_BLOCK = 384 + 384 + 192 + 12 + 192 * 8 + 4
+
+
+# The launches of one search-loop Compare pass (each kernel once; the other
+# entries above are the stage-dump path's or their fused parts).
+PASS_KERNELS = ("coeffs_to_linear", "opsin_mhic", "edge_mask", "block_diff", "blur_h", "blur_v",
+                "combine_channels", "diffmap_blur_h", "diffmap_blur_v", "diffmap_final")
 
 
 def region_bytes(name, w, h):
@@ -514,7 +523,7 @@ def main():
             blur_mask["traffic"] = int(sum(tr))
             blur_mask["traffic_GBps"] = round(sum(tr) / (bm_ms * 1e-3) / 1e9, 1)
     cp = prof.get("compare_pass")
-    pass_bytes = sum(bpp.values()) * w * h
+    pass_bytes = sum(bpp[k] for k in PASS_KERNELS) * w * h
     compare_pass = None
     if cp and cp[0]:
         avg = cp[1] / cp[0]
