@@ -133,6 +133,15 @@ bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
   return true;
 }
 
+// img holds exactly the q=1 originals resident on the device (d_orig_).
+bool HipButteraugliComparator::IsOriginal(const CoeffImage& img) const {
+  if (!orig_on_device_ || img.coeffs.size() != orig_.size()) return false;
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < kDCTBlockSize; ++k)
+      if (img.quant[c][k] != 1) return false;
+  return std::memcmp(img.coeffs.data(), orig_.data(), orig_.size() * sizeof(coeff_t)) == 0;
+}
+
 // Brings the device copy of the coefficients up to date with img: the
 // journalled edits when it is in img's epoch, else everything.
 bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
@@ -148,6 +157,10 @@ bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
     delta_val_.resize(n);
     for (size_t i = 0; i < n; ++i) delta_val_[i] = img.coeffs[idx[i]];
     ok = engine_->UploadCoeffDelta(idx, delta_val_.data(), n);
+  } else if (IsOriginal(img)) {
+    // the search's first image (CopyFromJpegData of the q=1 originals) is
+    // already resident: an HBM copy instead of a pageable upload
+    ok = engine_->CurrentFromOriginal();
   } else {
     ok = engine_->UploadCoeffs(img.coeffs.data());
   }

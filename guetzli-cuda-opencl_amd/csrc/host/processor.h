@@ -213,6 +213,7 @@ class HipButteraugliComparator : public Comparator {
   float distance_ = 0.0f;
   std::vector<float> block_max_;
   CoeffCursor device_;  // what the device copy of the coefficients reflects
+  bool IsOriginal(const CoeffImage& img) const;
   std::string cur_prologue_, kept_prologue_;  // headers of the encoded / kept candidates
   size_t cur_size_ = 0, kept_size_ = 0;
   std::string err_;

@@ -623,6 +623,15 @@ bool Engine::UploadCoeffs(const int16_t* coeffs) {
   return true;
 }
 
+bool Engine::CurrentFromOriginal() {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  cand_src_ = kCandCoeffs;
+  GZ_HIP(hipMemcpyAsync(d_cur_, d_orig_, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
+                        hipMemcpyDeviceToDevice, s));
+  return true;
+}
+
 bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));

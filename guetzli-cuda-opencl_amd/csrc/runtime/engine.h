@@ -80,6 +80,8 @@ class Engine {
   bool ComputeOriginalCoeffs(int16_t* host_out);
   // Candidate coefficients ([3][blocks][64]).
   bool UploadCoeffs(const int16_t* coeffs);
+  // The current coefficients <- the q=1 originals (an HBM copy, stream-ordered).
+  bool CurrentFromOriginal();
   // Applies coeffs[idx[i]] = val[i] to the device copy (stream-ordered before
   // the next pass): the search loop's per-iteration edits, a few 10k values.
   bool UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n);

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--quality", type=int, default=84)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--warmup", type=int, default=0,
+                    help="untimed encodes of the frame first (engine creation, first-touch)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -46,6 +48,9 @@ def main():
     w, h = args.width, args.height
     rgb = gz.synthetic_frame(args.seed, w, h)
     params = gz.Params.for_quality(args.quality)
+    for _ in range(args.warmup):
+        process_strips_once = gz.process_strips(rgb, w, h, coll, params, device=local)
+        del process_strips_once
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
@@ -63,7 +68,8 @@ def main():
            "rank0": {k: round(getattr(st, k), 3) for k in (
                "seconds_compare", "seconds_zeroing", "seconds_write", "seconds_quantize",
                "seconds_backend", "seconds_setup")},
-           "strip": gz.strip_layout(w, h, world, rank)}
+           "strip": gz.strip_layout(w, h, world, rank), "warmup": args.warmup,
+           "detail": gz.last_process_detail()}
     if args.check and world == 1:
         t1 = time.perf_counter()
         ref = gz.process(rgb, w, h, params, device=local)
