@@ -8,6 +8,8 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -854,6 +856,35 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   return true;
 }
 
+// The search's per-candidate waits.  Default: the runtime's own wait (it
+// polls).  GZ_WAIT_SPIN_US / GZ_WAIT_SLEEP_US (measurement knobs): poll for
+// SPIN_US, then sleep SLEEP_US between polls (timer slack 1 us on the
+// waiting thread), giving the host cores to other frames' back ends.
+template <class Query, class Block>
+static hipError_t HybridWait(Query query, Block block) {
+  static const long sleep_us = getenv("GZ_WAIT_SLEEP_US") ? atol(getenv("GZ_WAIT_SLEEP_US")) : 0;
+  static const long spin_us = getenv("GZ_WAIT_SPIN_US") ? atol(getenv("GZ_WAIT_SPIN_US")) : 0;
+  if (sleep_us <= 0) return block();
+  thread_local bool slack = false;
+  if (!slack) {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+    slack = true;
+  }
+  timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (;;) {
+    const hipError_t q = query();
+    if (q != hipErrorNotReady) return q;
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    const long el = (t.tv_sec - t0.tv_sec) * 1000000L + (t.tv_nsec - t0.tv_nsec) / 1000;
+    if (el >= spin_us) {
+      const timespec d = {0, sleep_us * 1000L};
+      nanosleep(&d, nullptr);
+    }
+  }
+}
+
 bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
@@ -898,7 +929,8 @@ bool Engine::CompareEnqueue() {
 }
 
 bool Engine::Sync() {
-  GZ_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream_)));
+  GZ_HIP(HybridWait([this] { return hipStreamQuery(static_cast<hipStream_t>(stream_)); },
+                    [this] { return hipStreamSynchronize(static_cast<hipStream_t>(stream_)); }));
   ProfFlush();
   return true;
 }
@@ -1222,7 +1254,8 @@ bool Engine::JpegStageEnqueue(const int q[3][64]) {
 }
 
 bool Engine::JpegStageWait(uint32_t* hist, uint64_t* chroma_nz) {
-  GZ_HIP(hipEventSynchronize(static_cast<hipEvent_t>(stage_event_)));
+  GZ_HIP(HybridWait([this] { return hipEventQuery(static_cast<hipEvent_t>(stage_event_)); },
+                    [this] { return hipEventSynchronize(static_cast<hipEvent_t>(stage_event_)); }));
   memcpy(hist, h_jhist_, 6 * 256 * 4);
   uint64_t nz;
   memcpy(&nz, h_jhist_ + 6 * 256, 8);
