@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -29,6 +31,20 @@ thread_local std::string g_last_detail = "{}";
 gz_status SetError(gz_status st, const std::string& msg) {
   g_last_error = msg;
   return st;
+}
+
+// No C++ exception may cross the C ABI (it would terminate the caller's
+// process): host allocation failure becomes GZ_ERR_OUT_OF_MEMORY, anything
+// else GZ_ERR_INTERNAL.
+template <class F>
+gz_status Guard(const char* what, F&& body) {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    return SetError(GZ_ERR_OUT_OF_MEMORY, std::string(what) + ": out of host memory");
+  } catch (const std::exception& e) {
+    return SetError(GZ_ERR_INTERNAL, std::string(what) + ": " + e.what());
+  }
 }
 
 }  // namespace
@@ -74,37 +90,41 @@ void gz_free(void* p) { std::free(p); }
 
 gz_status gz_png_decode(const uint8_t* png, size_t png_len, int* width, int* height,
                         uint8_t** rgb_out) {
-  if (!png || !width || !height || !rgb_out) return SetError(GZ_ERR_INVALID_ARG, "png_decode: bad argument");
-  std::vector<uint8_t> rgb;
-  std::string err;
-  int w = 0, h = 0;
-  if (!gz::ReadPng(png, png_len, &w, &h, &rgb, &err))
-    return SetError(GZ_ERR_INVALID_ARG, "png_decode: " + err);
-  uint8_t* buf = static_cast<uint8_t*>(std::malloc(rgb.size()));
-  if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "out of host memory");
-  std::memcpy(buf, rgb.data(), rgb.size());
-  *width = w;
-  *height = h;
-  *rgb_out = buf;
-  return GZ_OK;
+  return Guard("png_decode", [&]() -> gz_status {
+    if (!png || !width || !height || !rgb_out) return SetError(GZ_ERR_INVALID_ARG, "png_decode: bad argument");
+    std::vector<uint8_t> rgb;
+    std::string err;
+    int w = 0, h = 0;
+    if (!gz::ReadPng(png, png_len, &w, &h, &rgb, &err))
+      return SetError(GZ_ERR_INVALID_ARG, "png_decode: " + err);
+    uint8_t* buf = static_cast<uint8_t*>(std::malloc(rgb.size()));
+    if (!buf) return SetError(GZ_ERR_OUT_OF_MEMORY, "out of host memory");
+    std::memcpy(buf, rgb.data(), rgb.size());
+    *width = w;
+    *height = h;
+    *rgb_out = buf;
+    return GZ_OK;
+  });
 }
 
 gz_status gz_comparator_create(int device, int width, int height, const uint8_t* rgb,
                                float target_distance, gz_comparator** out) {
-  if (!out || !rgb || width < 8 || height < 8)
-    return SetError(GZ_ERR_INVALID_ARG, "gz_comparator_create: bad argument");
-  std::string err;
-  auto eng = gz::Engine::Create(device, width, height, &err);
-  if (!eng) return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + err);
-  if (!eng->SetReference(rgb, false))
-    return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + eng->error());
-  auto* c = new gz_comparator;
-  c->engine = std::move(eng);
-  c->target = target_distance;
-  c->w = width;
-  c->h = height;
-  *out = c;
-  return GZ_OK;
+  return Guard("gz_comparator_create", [&]() -> gz_status {
+    if (!out || !rgb || width < 8 || height < 8)
+      return SetError(GZ_ERR_INVALID_ARG, "gz_comparator_create: bad argument");
+    std::string err;
+    auto eng = gz::Engine::Create(device, width, height, &err);
+    if (!eng) return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + err);
+    if (!eng->SetReference(rgb, false))
+      return SetError(GZ_ERR_DEVICE, "gz_comparator_create: " + eng->error());
+    auto* c = new gz_comparator;
+    c->engine = std::move(eng);
+    c->target = target_distance;
+    c->w = width;
+    c->h = height;
+    *out = c;
+    return GZ_OK;
+  });
 }
 
 void gz_comparator_destroy(gz_comparator* cmp) { delete cmp; }
@@ -256,41 +276,45 @@ static gz_status CopyOut(const std::string& s, uint8_t** jpeg_out, size_t* jpeg_
 
 gz_status gz_comparator_write_jpeg(gz_comparator* cmp, const int16_t* coeffs, const int* quant,
                                    uint8_t** jpeg_out, size_t* jpeg_size) {
-  if (!cmp || !coeffs || !quant || !jpeg_out || !jpeg_size)
-    return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: bad argument");
-  int q[3][64];
-  for (int c = 0; c < 3; ++c)
-    for (int k = 0; k < 64; ++k) {
-      q[c][k] = quant[c * 64 + k];
-      if (q[c][k] < 1 || q[c][k] > 65535) return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: quant");
-    }
-  gz::Engine& e = *cmp->engine;
-  if (!e.UploadCoeffs(coeffs)) return SetError(GZ_ERR_DEVICE, "write_jpeg: " + e.error());
-  gz::JpegData meta;
-  std::string out, err;
-  if (!gz::DeviceWriteJpeg(&e, cmp->w, cmp->h, q, meta, true, &out, &err))
-    return SetError(GZ_ERR_DEVICE, "write_jpeg: " + err);
-  return CopyOut(out, jpeg_out, jpeg_size);
+  return Guard("write_jpeg", [&]() -> gz_status {
+    if (!cmp || !coeffs || !quant || !jpeg_out || !jpeg_size)
+      return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: bad argument");
+    int q[3][64];
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 64; ++k) {
+        q[c][k] = quant[c * 64 + k];
+        if (q[c][k] < 1 || q[c][k] > 65535) return SetError(GZ_ERR_INVALID_ARG, "write_jpeg: quant");
+      }
+    gz::Engine& e = *cmp->engine;
+    if (!e.UploadCoeffs(coeffs)) return SetError(GZ_ERR_DEVICE, "write_jpeg: " + e.error());
+    gz::JpegData meta;
+    std::string out, err;
+    if (!gz::DeviceWriteJpeg(&e, cmp->w, cmp->h, q, meta, true, &out, &err))
+      return SetError(GZ_ERR_DEVICE, "write_jpeg: " + err);
+    return CopyOut(out, jpeg_out, jpeg_size);
+  });
 }
 
 gz_status gz_write_jpeg_host(int width, int height, const int16_t* coeffs, const int* quant,
                              uint8_t** jpeg_out, size_t* jpeg_size) {
-  if (!coeffs || !quant || !jpeg_out || !jpeg_size || width <= 0 || height <= 0)
-    return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: bad argument");
-  gz::CoeffImage img;
-  img.Init(width, height);
-  std::memcpy(img.coeffs.data(), coeffs, img.coeffs.size() * sizeof(int16_t));
-  for (int c = 0; c < 3; ++c)
-    for (int k = 0; k < 64; ++k) {
-      img.quant[c][k] = quant[c * 64 + k];
-      if (img.quant[c][k] < 1 || img.quant[c][k] > 65535)
-        return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: quant");
-    }
-  gz::JpegData jpg;
-  img.SaveToJpegData(&jpg);
-  std::string out;
-  if (!gz::WriteJpegReference(jpg, true, &out)) return SetError(GZ_ERR_INTERNAL, "write_jpeg_host");
-  return CopyOut(out, jpeg_out, jpeg_size);
+  return Guard("write_jpeg_host", [&]() -> gz_status {
+    if (!coeffs || !quant || !jpeg_out || !jpeg_size || width <= 0 || height <= 0)
+      return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: bad argument");
+    gz::CoeffImage img;
+    img.Init(width, height);
+    std::memcpy(img.coeffs.data(), coeffs, img.coeffs.size() * sizeof(int16_t));
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 64; ++k) {
+        img.quant[c][k] = quant[c * 64 + k];
+        if (img.quant[c][k] < 1 || img.quant[c][k] > 65535)
+          return SetError(GZ_ERR_INVALID_ARG, "write_jpeg_host: quant");
+      }
+    gz::JpegData jpg;
+    img.SaveToJpegData(&jpg);
+    std::string out;
+    if (!gz::WriteJpegReference(jpg, true, &out)) return SetError(GZ_ERR_INTERNAL, "write_jpeg_host");
+    return CopyOut(out, jpeg_out, jpeg_size);
+  });
 }
 
 size_t gz_last_process_detail(char* buf, size_t cap) {
@@ -406,23 +430,25 @@ static gz_status ProcessImpl(int device, const gz_params* params, const uint8_t*
                              bool device_ptr, int w, int h, uint8_t** jpeg_out,
                              size_t* jpeg_size, gz_process_stats* stats,
                              const gz_collectives* coll = nullptr) {
-  if (!params || !rgb || !jpeg_out || !jpeg_size || w <= 0 || h <= 0)
-    return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
-  // (the strip decomposition of one frame runs the 4:4:4 search only)
-  if (coll && (params->try_420 || params->force_420))
-    return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output of a strip-decomposed frame is not supported");
-  const gz::ProcessParams pp = ToProcessParams(params);
-  gz::ProcessResult res;
-  std::string err;
-  int rc;
-  if (coll) {
-    CCollectives cc(coll);
-    rc = gz::ProcessStrips(device, pp, rgb, w, h, &cc, &res, &err);
-  } else {
-    rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
-  }
-  if (rc != 0) return SetError(rc, "process: " + err);
-  return Deliver(res, jpeg_out, jpeg_size, stats);
+  return Guard("process", [&]() -> gz_status {
+    if (!params || !rgb || !jpeg_out || !jpeg_size || w <= 0 || h <= 0)
+      return SetError(GZ_ERR_INVALID_ARG, "process: bad argument");
+    // (the strip decomposition of one frame runs the 4:4:4 search only)
+    if (coll && (params->try_420 || params->force_420))
+      return SetError(GZ_ERR_UNSUPPORTED, "process: 4:2:0 output of a strip-decomposed frame is not supported");
+    const gz::ProcessParams pp = ToProcessParams(params);
+    gz::ProcessResult res;
+    std::string err;
+    int rc;
+    if (coll) {
+      CCollectives cc(coll);
+      rc = gz::ProcessStrips(device, pp, rgb, w, h, &cc, &res, &err);
+    } else {
+      rc = gz::Process(device, pp, rgb, device_ptr, w, h, &res, &err);
+    }
+    if (rc != 0) return SetError(rc, "process: " + err);
+    return Deliver(res, jpeg_out, jpeg_size, stats);
+  });
 }
 
 // The encoded bytes (library-allocated) and statistics of a finished encode.
@@ -472,46 +498,50 @@ gz_status gz_process_rgb_device(int device, const gz_params* params, const uint8
 
 gz_status gz_process_jpeg(int device, const gz_params* params, const uint8_t* jpeg, size_t jpeg_len,
                           uint8_t** jpeg_out, size_t* jpeg_size, gz_process_stats* stats) {
-  if (!params || !jpeg || !jpeg_out || !jpeg_size)
-    return SetError(GZ_ERR_INVALID_ARG, "process_jpeg: bad argument");
-  gz::ProcessResult res;
-  std::string err;
-  const int rc = gz::ProcessJpeg(device, ToProcessParams(params), jpeg, jpeg_len, &res, &err);
-  if (rc != 0) return SetError(rc, "process_jpeg: " + err);
-  return Deliver(res, jpeg_out, jpeg_size, stats);
+  return Guard("process_jpeg", [&]() -> gz_status {
+    if (!params || !jpeg || !jpeg_out || !jpeg_size)
+      return SetError(GZ_ERR_INVALID_ARG, "process_jpeg: bad argument");
+    gz::ProcessResult res;
+    std::string err;
+    const int rc = gz::ProcessJpeg(device, ToProcessParams(params), jpeg, jpeg_len, &res, &err);
+    if (rc != 0) return SetError(rc, "process_jpeg: " + err);
+    return Deliver(res, jpeg_out, jpeg_size, stats);
+  });
 }
 
 gz_status gz_jpeg_decode(const uint8_t* jpeg, size_t jpeg_len, int* width, int* height,
                          int* ncomp, int16_t** coeffs_out, size_t* ncoeffs, uint8_t** rgb_out) {
-  if (!jpeg || !width || !height || !ncomp || !coeffs_out || !ncoeffs || !rgb_out)
-    return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: bad argument");
-  *coeffs_out = nullptr;
-  *rgb_out = nullptr;
-  gz::JpegData jpg;
-  std::string err;
-  if (!gz::ReadJpeg(jpeg, jpeg_len, &jpg, &err)) return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: " + err);
-  *width = jpg.width;
-  *height = jpg.height;
-  *ncomp = static_cast<int>(jpg.components.size());
-  size_t n = 0;
-  for (const auto& c : jpg.components) n += c.coeffs.size();
-  int16_t* co = static_cast<int16_t*>(std::malloc(n ? n * sizeof(int16_t) : 1));
-  if (!co) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
-  size_t at = 0;
-  for (const auto& c : jpg.components) {
-    std::memcpy(co + at, c.coeffs.data(), c.coeffs.size() * sizeof(int16_t));
-    at += c.coeffs.size();
-  }
-  *coeffs_out = co;
-  *ncoeffs = n;
-  std::vector<uint8_t> rgb;
-  if (gz::DecodeJpegToRGB(jpg, &rgb)) {
-    uint8_t* r = static_cast<uint8_t*>(std::malloc(rgb.size()));
-    if (!r) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
-    std::memcpy(r, rgb.data(), rgb.size());
-    *rgb_out = r;
-  }
-  return GZ_OK;
+  return Guard("jpeg_decode", [&]() -> gz_status {
+    if (!jpeg || !width || !height || !ncomp || !coeffs_out || !ncoeffs || !rgb_out)
+      return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: bad argument");
+    *coeffs_out = nullptr;
+    *rgb_out = nullptr;
+    gz::JpegData jpg;
+    std::string err;
+    if (!gz::ReadJpeg(jpeg, jpeg_len, &jpg, &err)) return SetError(GZ_ERR_INVALID_ARG, "jpeg_decode: " + err);
+    *width = jpg.width;
+    *height = jpg.height;
+    *ncomp = static_cast<int>(jpg.components.size());
+    size_t n = 0;
+    for (const auto& c : jpg.components) n += c.coeffs.size();
+    int16_t* co = static_cast<int16_t*>(std::malloc(n ? n * sizeof(int16_t) : 1));
+    if (!co) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
+    size_t at = 0;
+    for (const auto& c : jpg.components) {
+      std::memcpy(co + at, c.coeffs.data(), c.coeffs.size() * sizeof(int16_t));
+      at += c.coeffs.size();
+    }
+    *coeffs_out = co;
+    *ncoeffs = n;
+    std::vector<uint8_t> rgb;
+    if (gz::DecodeJpegToRGB(jpg, &rgb)) {
+      uint8_t* r = static_cast<uint8_t*>(std::malloc(rgb.size()));
+      if (!r) return SetError(GZ_ERR_OUT_OF_MEMORY, "jpeg_decode: out of host memory");
+      std::memcpy(r, rgb.data(), rgb.size());
+      *rgb_out = r;
+    }
+    return GZ_OK;
+  });
 }
 
 gz_status gz_process_rgb_strips(int device, const gz_params* params, const uint8_t* rgb, int width,

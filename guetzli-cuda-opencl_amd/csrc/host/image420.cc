@@ -1,3 +1,10 @@
+// Portions restate Guetzli (Copyright 2016 Google Inc., Apache License 2.0,
+// http://www.apache.org/licenses/LICENSE-2.0) as modified in
+// yyamamoto79/guetzli-cuda-opencl: preprocess_downsample.cc (PreProcessChannel, Sharpen, Erode, Dilate,
+// RGBToYUV420), output_image.cc (the factor-2 SetCoeffBlock / Downsample /
+// SaveToJpegData) and dct_double.cc.
+// Byte-exact output forces their operation order and constants; the
+// code around them is this repository's own.
 #include "host/image420.h"
 
 #include <algorithm>

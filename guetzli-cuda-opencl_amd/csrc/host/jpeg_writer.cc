@@ -1,3 +1,9 @@
+// Portions restate Guetzli (Copyright 2016 Google Inc., Apache License 2.0,
+// http://www.apache.org/licenses/LICENSE-2.0) as modified in
+// yyamamoto79/guetzli-cuda-opencl: jpeg_data_writer.cc and entropy_encode.cc (SetDepth /
+// ClusterHistograms / the Huffman code construction).
+// Byte-exact output forces their operation order and constants; the
+// code around them is this repository's own.
 #include "host/jpeg_writer.h"
 
 #include <algorithm>

@@ -228,6 +228,11 @@ bool ReadPng(const uint8_t* data, size_t size, int* width, int* height, std::vec
   }
   size_t need = 0;
   for (const Pass& ps : passes) need += ps.ph * (1 + ps.stride);
+  // deflate expands at most 1032:1 (258-byte matches coded in 2 bits), so a
+  // header promising more than that cannot be backed by this IDAT data:
+  // libpng ends such a file with "not enough image data"; failing before
+  // allocating keeps a tiny file from asking for terabytes
+  if (need / 1032 > z.size() + 64) return Fail(err, "PNG image data error");
   std::vector<uint8_t> raw;
   if (!Inflate(z, need, &raw)) return Fail(err, "PNG image data error");
   // samples after EXPAND / STRIP_16: out_ch 8-bit values per pixel

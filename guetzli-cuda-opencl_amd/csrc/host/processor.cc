@@ -1,3 +1,9 @@
+// Portions restate Guetzli (Copyright 2016 Google Inc., Apache License 2.0,
+// http://www.apache.org/licenses/LICENSE-2.0) as modified in
+// yyamamoto79/guetzli-cuda-opencl: processor.cc, quality.cc, score.cc and butteraugli_comparator.cc
+// (QuantMatrixGenerator, the back end's control flow, kLocalMaxWeight).
+// Byte-exact output forces their operation order and constants; the
+// code around them is this repository's own.
 // The Guetzli search loop on the host (guetzli/processor.cc), driving the GPU
 // comparator.  Control flow, heuristics and every floating-point decision are
 // those of the reference's CPU_OPT (`guetzli --c`) path so the output bytes
@@ -1014,8 +1020,8 @@ class Processor {
   }
   bool TryQuantMatrix(const JpegData& jpg_in, float target_mul, const int q[3][kDCTBlockSize],
                       CoeffImage* img, QuantData* data, std::string* err);
-  bool SelectQuantMatrix(const JpegData& jpg_in, int best_q[3][kDCTBlockSize], CoeffImage* img,
-                         bool* ok, std::string* err);
+  bool SelectQuantMatrix(const JpegData& jpg_in, bool downsample, int best_q[3][kDCTBlockSize],
+                         CoeffImage* img, bool* ok, std::string* err);
   bool SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int comp_mask,
                               double target_mul, bool stop_early, std::string* err);
   bool SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int comp_mask,
@@ -1063,10 +1069,11 @@ bool Processor::TryQuantMatrix(const JpegData& jpg_in, float target_mul,
   return true;
 }
 
-bool Processor::SelectQuantMatrix(const JpegData& jpg_in, int best_q[3][kDCTBlockSize],
-                                  CoeffImage* img, bool* ok, std::string* err) {
+bool Processor::SelectQuantMatrix(const JpegData& jpg_in, bool downsample,
+                                  int best_q[3][kDCTBlockSize], CoeffImage* img, bool* ok,
+                                  std::string* err) {
   // processor.cc:340-372
-  QuantMatrixGenerator qgen;
+  QuantMatrixGenerator qgen(downsample);
   const float target_mul_high = 0.97f, target_mul_low = 0.95f;
   QuantData best;
   if (!TryQuantMatrix(jpg_in, target_mul_high, best_q, img, &best, err)) return false;
@@ -1381,7 +1388,6 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       res_->detail["backend_sort_s"] += sort_s;
       res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += changed_coeffs;
-      if (getenv("GZ_DEBUG_BACKEND")) fprintf(stderr, "iter dir %d n %zu min %d bulk %zu changed %d thr %.9g est %d prev %d\n", direction, n_order, min_coeffs_to_change, bulk, changed_coeffs, val_threshold, est_jpg_size, prev_size);
       for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
@@ -1510,22 +1516,36 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
   }
   const int try_420 = (input_is_420 || params_.force_420 || (params_.try_420 && !IsGrayscale(jpg_in))) ? 1 : 0;
   const int force_420 = (input_is_420 || params_.force_420) ? 1 : 0;
+  // DownsampleImage leaves an image whose chroma is all zero at 4:4:4
+  // (output_image.cc:535-539) and SaveToJpegData keeps its one component, so
+  // the "4:2:0" pass of such an image is the 4:4:4 machinery on a
+  // one-component JpegData: the downsampling quantization generator, then the
+  // Y search alone with ymul 1.0 (processor.cc:994-1016).
+  const bool gray_pass = !input_is_420 && IsGrayscale(jpg);
   for (int downsample = force_420; downsample <= try_420; ++downsample) {
-    if (downsample) {
+    if (downsample && !gray_pass) {
       const int rc = Run420(jpg_in, err);
       if (rc != GZ_OK) return rc;
       continue;
+    }
+    JpegData gray;
+    const JpegData* pass_jpg = &jpg;
+    if (downsample) {
+      gray = jpg;
+      gray.components.resize(1);
+      pass_jpg = &gray;
     }
     img.CopyFromJpegData(jpg);
     int best_q[3][kDCTBlockSize];
     std::memcpy(best_q, q_in, sizeof(best_q));
     bool ok = false;
-    if (!SelectQuantMatrix(jpg, best_q, &img, &ok, err)) return GZ_ERR_DEVICE;
+    if (!SelectQuantMatrix(*pass_jpg, downsample != 0, best_q, &img, &ok, err)) return GZ_ERR_DEVICE;
     if (!ok)
       for (int c = 0; c < 3; ++c)
         for (int i = 0; i < kDCTBlockSize; ++i) best_q[c][i] = 1;
     if (!cmp_->QuantizeFromOriginal(best_q, &img)) return device_error();
-    if (!SelectFrequencyMasking(jpg, &img, 7, 1.0, false, err)) return GZ_ERR_DEVICE;
+    if (!SelectFrequencyMasking(*pass_jpg, &img, downsample ? 1 : 7, 1.0, false, err))
+      return GZ_ERR_DEVICE;
   }
   FlushOutput();
   if (kept_on_device_ && !cmp_->DeviceFetchKept(&res_->jpeg)) return device_error();
@@ -1826,6 +1846,12 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
     if (err) *err = "Could not create jpg data from rgb pixels";
     return GZ_ERR_INVALID_ARG;
   }
+  if (params.butteraugli_target > 2.0f) {
+    // ProcessJpegData's first check (processor.cc:939-945), made before any
+    // device work so that the answer does not depend on a device being there
+    if (err) *err = "butteraugli target above 2.0 (quality below 84) is not supported";
+    return GZ_ERR_INVALID_ARG;
+  }
   JpegData jpg;
   std::unique_ptr<HipButteraugliComparator> cmp;
   if (w >= 32 && h >= 32) {
@@ -1880,8 +1906,12 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     if (err) *err = "Unsupported input JPEG (unexpectedly large coefficient values)";
     return GZ_ERR_INVALID_ARG;
   }
-  // ProcessJpegData's input checks (processor.cc:946-963), ahead of the
+  // ProcessJpegData's input checks (processor.cc:939-963), ahead of the
   // decode
+  if (params.butteraugli_target > 2.0f) {
+    if (err) *err = "butteraugli target above 2.0 (quality below 84) is not supported";
+    return GZ_ERR_INVALID_ARG;
+  }
   if (jpg.components.size() != 3 || !HasYCbCrColorSpace(jpg)) {
     if (err) *err = "Only YUV color space input jpeg is supported";
     return GZ_ERR_UNSUPPORTED;

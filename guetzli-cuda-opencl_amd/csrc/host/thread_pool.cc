@@ -1,5 +1,7 @@
 #include "host/thread_pool.h"
 
+#include <sched.h>
+
 #include <pthread.h>
 #include <stdio.h>
 #include <time.h>
@@ -118,11 +120,18 @@ Pool* GetPool() {
 }  // namespace
 
 namespace {
-// CPUs this process may use: the affinity set, capped by a cgroup v2 CPU
-// quota (cpu.max "quota period"; a container's CPU share is often a quota,
-// not an affinity mask).
-int UsableCpus() {
-  int n = static_cast<int>(std::thread::hardware_concurrency());
+// CPUs this process may use: its affinity set (sched_getaffinity), capped by
+// a cgroup v2 CPU quota (cpu.max "quota period"; a container's CPU share is
+// often a quota, not an affinity mask).  *pinned: the affinity set is smaller
+// than the online CPUs, i.e. someone (taskset, numactl, a launcher) already
+// gave this process its share.
+int UsableCpus(bool* pinned) {
+  const int online = std::max(1, static_cast<int>(std::thread::hardware_concurrency()));
+  int n = online;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = CPU_COUNT(&set);
+  *pinned = n < online;
   if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
     char quota[32] = {0};
     long period = 0;
@@ -141,10 +150,12 @@ int HostThreads() {
     const char* e = std::getenv("GZ_HOST_THREADS");
     if (e && std::atoi(e) > 0) return std::min(256, std::atoi(e));
     // the node's CPUs shared by the ranks on it (torch.distributed.run sets
-    // LOCAL_WORLD_SIZE), at most 16 per process
-    int share = UsableCpus();
+    // LOCAL_WORLD_SIZE) unless this rank is pinned to its own cpuset, at
+    // most 16 per process
+    bool pinned = false;
+    int share = UsableCpus(&pinned);
     const char* lw = std::getenv("LOCAL_WORLD_SIZE");
-    if (lw && std::atoi(lw) > 1) share /= std::atoi(lw);
+    if (!pinned && lw && std::atoi(lw) > 1) share /= std::atoi(lw);
     return std::max(1, std::min(16, share));
   }();
   return n;

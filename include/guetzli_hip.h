@@ -50,8 +50,12 @@ typedef struct {
 
 /* guetzli::Params (guetzli/processor.h:34-42); same defaults via
  * gz_params_init().  try_420 / force_420 / use_silver_screen run the 4:2:0
- * pass of ProcessJpegData (processor.cc:986-1016); the strip decomposition of
- * one frame (gz_process_rgb_strips) supports the 4:4:4 search only. */
+ * pass of ProcessJpegData (processor.cc:986-1016); on an image whose chroma
+ * is all zero that pass keeps one component at 4:4:4, as the reference does
+ * (output_image.cc:535-539).  A butteraugli_target above 2.0 (quality below
+ * 84) returns GZ_ERR_INVALID_ARG (processor.cc:939-945).  The strip
+ * decomposition of one frame (gz_process_rgb_strips) supports the 4:4:4
+ * search only. */
 typedef struct {
   float butteraugli_target;
   int clear_metadata;
@@ -107,7 +111,9 @@ double gz_butteraugli_score_for_quality(double quality);
 void gz_free(void* p);
 
 /* ---- encode (guetzli::Process, guetzli/processor.h:62-64) -------------- */
-/* Encodes an RGB image; *jpeg_out is allocated by the library (gz_free). */
+/* Encodes an RGB image; *jpeg_out is allocated by the library (gz_free).
+ * Images under 32 pixels in either dimension are written at quantization 1
+ * without a search and without device work (processor.cc:1170-1181). */
 gz_status gz_process_rgb(int device, const gz_params* params, const uint8_t* rgb, int width,
                          int height, uint8_t** jpeg_out, size_t* jpeg_size,
                          gz_process_stats* stats);

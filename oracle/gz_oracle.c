@@ -9,6 +9,10 @@
  * expression that contains a double literal is evaluated in double and
  * rounded once on assignment to float.  Transcendental tables (blur taps,
  * sRGB, mask LUTs) use glibc exp/pow in double, as the reference does.
+ *
+ * The algorithms restated are Guetzli's and Butteraugli's (Copyright 2016
+ * Google Inc., Apache License 2.0) as modified in
+ * yyamamoto79/guetzli-cuda-opencl (clguetzli/clbutter_comparator.cpp).
  */
 #include "gz_oracle.h"
 

@@ -102,15 +102,25 @@ def run_zero_variants():
 
 
 def run_e2e(manifest, cases, section="e2e"):
-    """cases: (name, rgb path, w, h, quality[, {Params overrides}])."""
+    """cases: (name, rgb path, w, h, quality[, {Params overrides}]).  A case
+    whose reference run returns false (guetzli::Process, exit status 3 of the
+    driver) is recorded as {"fail": true}."""
     out = manifest.setdefault(section, {})
     for case in cases:
         name, rgb, w, h, q = case[:5]
         params = case[5] if len(case) > 5 else {}
         jpg = "/tmp/gz_fixture_%s.jpg" % name
         res = subprocess.run([REF, "encode", rgb, str(w), str(h), str(q), jpg, "c"] +
-                             ["%s=%d" % kv for kv in sorted(params.items())], check=True,
+                             ["%s=%d" % kv for kv in sorted(params.items())],
                              capture_output=True, text=True)
+        if res.returncode == 3:
+            out[name] = {"w": w, "h": h, "quality": q, "fail": True,
+                         "input": os.path.relpath(rgb, HERE) if rgb.startswith(HERE) else rgb}
+            if params:
+                out[name]["params"] = params
+            print(section, name, out[name])
+            continue
+        res.check_returncode()
         info = json.loads(res.stdout)
         out[name] = {"w": w, "h": h, "quality": q, "sha256": sha256(jpg), "bytes": info["bytes"],
                      "iters": info["iters"], "ref_seconds": info["seconds"],
@@ -171,6 +181,48 @@ def main():
             cases.append(("%s_q%d_%s%s" % (name, q, "try420" if "try_420" in params else "force420",
                                            "_" + tag if tag else ""), rgb, w, h, q, params))
         run_e2e(manifest, cases, section="e2e_420")
+    if "e2e-edge" in what:
+        # the reference's edge paths (processor.cc):
+        #  - images under 32 px in either dimension: no comparator, the q=1
+        #    encode is the output (:1170-1181 -> :971-977);
+        #  - quality below 84 (target above 2.0): Process returns false (:939-945);
+        #  - force_420 on content whose chroma is all zero: Downsample leaves
+        #    the image at 4:4:4 (output_image.cc:535-539), SaveToJpegData keeps
+        #    one component, and the pass runs the downsampling quantization
+        #    generator with comp_mask 1 and ymul 1.0 (:991-1016);
+        #  - try_420 on such content: IsGrayscale skips the 4:2:0 pass (:986-988).
+        d = os.path.join(HERE, "edge")
+        os.makedirs(d, exist_ok=True)
+
+        def save(name, img):
+            path = os.path.join(d, name + ".rgb")
+            np.ascontiguousarray(img).tofile(path)
+            h, w, _ = img.shape
+            return path, w, h
+
+        def gray(img):
+            g = img[:, :, 1:2]
+            return np.repeat(g, 3, axis=2)
+
+        cases = []
+        for name, (w, h), seed in [("tex_24x24", (24, 24), 21), ("tex_300x20", (300, 20), 22),
+                                   ("tex_20x300", (20, 300), 23), ("tex_31x64", (31, 64), 24),
+                                   ("tex_1x1", (1, 1), 25)]:
+            path, w, h = save(name, texture_image(w, h, seed) if w * h > 1 else
+                              np.full((1, 1, 3), 77, np.uint8))
+            cases.append(("%s_q95" % name, path, w, h, 95))
+        tex = save("tex_64x48", texture_image(64, 48, 26))
+        cases.append(("tex_64x48_q80", tex[0], tex[1], tex[2], 80))
+        small = os.path.join(d, "tex_24x24.rgb")
+        cases.append(("tex_24x24_q83", small, 24, 24, 83))
+        g1 = save("gray_96x64", gray(texture_image(96, 64, 27)))
+        g2 = save("gray_bees_88x64", gray(bees_crop(120, 60, 88, 64)))
+        cases += [("gray_96x64_q95_force420", g1[0], g1[1], g1[2], 95, {"force_420": 1}),
+                  ("gray_96x64_q90_force420", g1[0], g1[1], g1[2], 90, {"force_420": 1}),
+                  ("gray_bees_88x64_q95_force420", g2[0], g2[1], g2[2], 95, {"force_420": 1}),
+                  ("gray_96x64_q95_try420", g1[0], g1[1], g1[2], 95, {"try_420": 1}),
+                  ("gray_bees_88x64_q95", g2[0], g2[1], g2[2], 95)]
+        run_e2e(manifest, cases, section="e2e_edge")
     if "e2e-420-1080" in what:
         # the 4:2:0 pass at full size: synthetic 1920x1080 seed 0 (the bench's
         # frame), q95, force_420 -- about 7 minutes of reference CPU time

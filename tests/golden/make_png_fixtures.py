@@ -160,6 +160,12 @@ def cases():
     bad = good[:crc_at] + bytes([good[crc_at] ^ 0x55]) + good[crc_at + 1:]
     out.append(("bad_crc", bad))
     out.append(("truncated", good[:len(good) // 2]))
+    # a header promising 30000 x 30000 RGB (2.7 GB of scanlines) over a few
+    # bytes of IDAT: libpng runs out of image data; a reader must not size its
+    # buffers from the header alone
+    huge = (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", 30000, 30000, 8, 2, 0, 0, 0))
+            + chunk(b"IDAT", zlib.compress(b"\x00" * 4000)) + chunk(b"IEND", b""))
+    out.append(("huge_ihdr", huge))
     return out
 
 

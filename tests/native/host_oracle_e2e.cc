@@ -38,6 +38,8 @@ int main(int argc, char** argv) {
     const int v = atoi(kv.c_str() + eq + 1);
     if (kv.compare(0, eq, "lookahead") == 0) params.zeroing_greedy_lookahead = v;
     else if (kv.compare(0, eq, "new_model") == 0) params.new_zeroing_model = v != 0;
+    else if (kv.compare(0, eq, "force_420") == 0) params.force_420 = v != 0;
+    else if (kv.compare(0, eq, "try_420") == 0) params.try_420 = v != 0;
     else return 1;
   }
   gz::JpegData jpg;

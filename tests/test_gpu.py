@@ -360,3 +360,24 @@ def test_device_coded_original_output_matches_host_writer(gz, kind, monkeypatch)
         rgb = np.ascontiguousarray(np.repeat(g, 3, axis=2)).reshape(-1)
     data = gz.process(rgb, w, h, gz.Params.for_quality(95))
     assert data[:2] == b"\xff\xd8"
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST.get("e2e_edge", {})))
+def test_process_edge_known_answers(gz, name):
+    """The reference's edge paths on the device path: images under 32 px
+    (no comparator), quality below 84 (refused), force_420 / try_420 on
+    content whose chroma is all zero (the one-component continuation with
+    the downsampling quantization generator, processor.cc:986-1016)."""
+    e = MANIFEST["e2e_edge"][name]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    p = gz.Params.for_quality(e["quality"])
+    p.force_420 = bool(e.get("params", {}).get("force_420", 0))
+    p.try_420 = bool(e.get("params", {}).get("try_420", 0))
+    if e.get("fail"):
+        with pytest.raises(gz.GuetzliError) as err:
+            gz.process(rgb, e["w"], e["h"], p)
+        assert err.value.status == 1
+        return
+    data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
+    assert st.iterations == e["iters"]
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]

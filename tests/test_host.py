@@ -87,16 +87,27 @@ def _e2e_params_cases():
             if e["w"] * e["h"] <= 100 * 100]
 
 
-@pytest.mark.parametrize("section,name", [("e2e", n) for n in _e2e_cases()] + _e2e_params_cases())
+def _e2e_edge_cases():
+    return [("e2e_edge", n) for n in sorted(MANIFEST.get("e2e_edge", {}))]
+
+
+@pytest.mark.parametrize("section,name", [("e2e", n) for n in _e2e_cases()] + _e2e_params_cases()
+                         + _e2e_edge_cases())
 def test_host_loop_with_oracle_comparator_bit_exact(host_e2e_bin, section, name, tmp_path):
     """Product host loop + CPU-oracle comparator == the reference's bytes,
-    including the Params variants (old zeroing model, lookahead 1 / 2)."""
+    including the Params variants (old zeroing model, lookahead 1 / 2) and
+    the edge paths (images under 32 px, quality below 84, force_420 on
+    content without chroma)."""
     e = MANIFEST[section][name]
     out = tmp_path / "out.jpg"
     res = subprocess.run([host_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]), str(e["h"]),
                           str(e["quality"]), str(out)] +
                          ["%s=%d" % kv for kv in sorted(e.get("params", {}).items())],
                          capture_output=True, text=True, timeout=600)
+    if e.get("fail"):
+        # guetzli::Process returns false (processor.cc:939-945)
+        assert res.returncode == 3 and "2.0" in res.stderr, res.stderr
+        return
     assert res.returncode == 0, res.stderr
     info = json.loads(res.stdout)
     assert info["iters"] == e["iters"]
@@ -160,3 +171,23 @@ def test_no_cpu_fallback_without_gpu(gz, gpu_available):
     with pytest.raises(gz.GuetzliError) as e:
         gz.process(rgb, 64, 64, gz.Params.for_quality(95))
     assert e.value.status == 2
+
+
+@pytest.mark.parametrize("name", sorted(n for n, e in MANIFEST.get("e2e_edge", {}).items()
+                                        if e.get("fail") or e["w"] < 32 or e["h"] < 32))
+def test_process_edge_paths_without_device(gz, name):
+    """The two edge paths of guetzli::Process that need no Butteraugli,
+    through the product's C ABI: images under 32 px in either dimension get
+    the q=1 encode as their output (processor.cc:1170-1181 -> :971-977), and
+    quality below 84 is refused (:939-945) -- with or without a device."""
+    e = MANIFEST["e2e_edge"][name]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    p = gz.Params.for_quality(e["quality"])
+    if e.get("fail"):
+        with pytest.raises(gz.GuetzliError) as err:
+            gz.process(rgb, e["w"], e["h"], p)
+        assert err.value.status == 1
+        return
+    data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
+    assert st.iterations == e["iters"] == 0
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]
