@@ -30,6 +30,7 @@
 #include "host/jpeg_reader.h"
 #include "host/jpeg_writer.h"
 #include "host/lazy_sort.h"
+#include "host/strips.h"
 #include "host/thread_pool.h"
 
 namespace gz {
@@ -214,23 +215,9 @@ int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram
     if (err) *err = e->error();
     return -1;
   }
-  const int ncomp = chroma > 0 ? 3 : 1;  // SaveToJpegData drops all-zero chroma
-  for (int c = 0; c < 3; ++c) {
-    dc[c].Clear();
-    ac[c].Clear();
-    if (c >= ncomp) continue;
-    for (int i = 0; i < 256; ++i) {
-      dc[c].counts[i] = 2 * hist[(2 * c) * 256 + i];
-      ac[c].counts[i] = 2 * hist[(2 * c + 1) * 256 + i];
-    }
-  }
-  return ncomp;
+  return HistogramsFromStage(hist, chroma, dc, ac);
 }
 
-namespace {
-// Staged histograms (6 x 256 counts, chroma non-zero count) -> per-component
-// DC / AC histograms as SaveToJpegData stores them; returns the component
-// count.
 int HistogramsFromStage(const uint32_t* hist, uint64_t chroma, JpegHistogram dc[3],
                         JpegHistogram ac[3]) {
   const int ncomp = chroma > 0 ? 3 : 1;  // SaveToJpegData drops all-zero chroma
@@ -246,8 +233,6 @@ int HistogramsFromStage(const uint32_t* hist, uint64_t chroma, JpegHistogram dc[
   return ncomp;
 }
 
-// Headers (*prologue) and Huffman code tables of an image with these
-// histograms (WriteJpeg's table choice, jpeg_data_writer.cc).
 bool PrepareScanFor(const JpegData& hdr, bool strip_metadata, int ncomp, JpegHistogram* dc_h,
                     JpegHistogram* ac_h, std::string* prologue, JpegCodeTables* codes) {
   HuffCodeTable dc_tab[3], ac_tab[3];
@@ -273,32 +258,17 @@ bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& me
   JpegHeaderFor(w, h, q, ncomp, &hdr);
   return PrepareScanFor(hdr, strip_metadata, ncomp, dc_h, ac_h, prologue, codes);
 }
-}  // namespace
 
 bool DeviceEncodeJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
                       bool strip_metadata, std::string* prologue, size_t* size, std::string* err) {
   JpegHistogram dc_h[3], ac_h[3];
   const int ncomp = DeviceJpegHistograms(e, q, dc_h, ac_h, err);
   if (ncomp < 0) return false;
-  JpegData hdr;
-  hdr.app_data = meta.app_data;
-  hdr.com_data = meta.com_data;
-  JpegHeaderFor(w, h, q, ncomp, &hdr);
-  HuffCodeTable dc_tab[3], ac_tab[3];
-  prologue->clear();
-  if (!WriteJpegPrologue(hdr, strip_metadata, dc_h, ac_h, dc_tab, ac_tab, prologue)) {
+  JpegCodeTables codes;
+  if (!PrepareScan(w, h, q, meta, strip_metadata, ncomp, dc_h, ac_h, prologue, &codes)) {
     if (err) *err = "jpeg header";
     return false;
   }
-  JpegCodeTables codes;
-  std::memset(&codes, 0, sizeof(codes));
-  for (int c = 0; c < ncomp; ++c)
-    for (int i = 0; i < 256; ++i) {
-      codes.dc_len[c][i] = dc_tab[c].depth[i];
-      codes.ac_len[c][i] = ac_tab[c].depth[i];
-      codes.dc_code[c][i] = static_cast<uint16_t>(dc_tab[c].code[i]);
-      codes.ac_code[c][i] = static_cast<uint16_t>(ac_tab[c].code[i]);
-    }
   uint64_t nbits = 0, ff = 0;
   if (!e->JpegScan(ncomp, codes, &nbits, &ff)) {
     if (err) *err = e->error();
@@ -834,8 +804,10 @@ struct AcBlockModel {
   // weight * symbols of the segment after non-zero position p (0 = none /
   // DC) through the non-zeros `mid` (0: none) and `nx` (0: none; then EOB
   // if the last one is below 63).
+  // H: the histogram (JpegHistogram) or a recorder of the same Add calls.
+  template <class H>
   static void Segment(int weight, int p, int mid, int mid_size, int nx, int nx_size,
-                      const uint8_t* depth, JpegHistogram* h, int64_t* raw) {
+                      const uint8_t* depth, H* h, int64_t* raw) {
     int last = p;
     int64_t bits = 0;
     auto put = [&](int pos, int size) {
@@ -861,8 +833,9 @@ struct AcBlockModel {
   }
 
   // block[k] := newval with the histogram / raw-bit bookkeeping.
+  template <class H>
   void Change(int c, int bix, int blocks, coeff_t* block, int k, coeff_t newval, const int* q,
-              const uint8_t* depth, JpegHistogram* h, int64_t* raw) {
+              const uint8_t* depth, H* h, int64_t* raw) {
     const coeff_t old = block[k];
     block[k] = newval;
     const int z = kJPEGZigZagOrder[k];
@@ -878,6 +851,19 @@ struct AcBlockModel {
     Segment(1, p, newval ? z : 0, newval ? SizeInv(newval, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h,
             raw);
     if (newval) m |= 1ull << z; else m &= ~(1ull << z);
+  }
+};
+
+// The symbol updates of one change, as the partitioned back end publishes
+// them (the AcBlockModel::Change calls recorded instead of applied).
+struct SymbolLog {
+  uint8_t n = 0;
+  uint8_t sym[32];
+  int8_t weight[32];
+  void Add(int s, int w) {
+    sym[n] = static_cast<uint8_t>(s);
+    weight[n] = static_cast<int8_t>(w);
+    ++n;
   }
 };
 
@@ -906,8 +892,8 @@ size_t EntropyCodedDataSize(const std::vector<JpegHistogram>& histograms,
 
 class Processor {
  public:
-  Processor(const ProcessParams& p, Comparator* cmp, ProcessResult* res)
-      : params_(p), cmp_(cmp), res_(res), scratch_(NewScanScratch(), FreeScanScratch) {}
+  Processor(const ProcessParams& p, Comparator* cmp, ProcessResult* res, Partition* part)
+      : params_(p), cmp_(cmp), res_(res), part_(part), scratch_(NewScanScratch(), FreeScanScratch) {}
   ~Processor() {
     if (writer_.joinable()) writer_.join();
   }
@@ -1028,6 +1014,8 @@ class Processor {
                               double target_mul, bool stop_early,
                               const std::vector<int>& offsets, const std::vector<uint8_t>& coeffs,
                               const std::vector<float>& errors, std::string* err);
+  bool GatherEntries(std::vector<std::pair<int, float>>* entries, int own_lo, int own_hi, int gbase,
+                     int* blocks_to_change);
   // The 4:2:0 pass (processor.cc:989-1016, downsample = 1) on the host model
   // Image420, entropy coded on the host.
   int Run420(const JpegData& jpg_in, std::string* err);
@@ -1039,6 +1027,7 @@ class Processor {
   ProcessParams params_;
   Comparator* cmp_;
   ProcessResult* res_;
+  Partition* part_;  // nullptr: the whole frame is this process's
   std::unique_ptr<ScanScratch, void (*)(ScanScratch*)> scratch_;
   std::thread writer_;
   std::string pending_;
@@ -1115,12 +1104,21 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
                                        const std::vector<int>& offsets,
                                        const std::vector<uint8_t>& cand,
                                        const std::vector<float>& cand_err, std::string* err) {
-  // processor.cc:723-919
+  // processor.cc:723-919.  With a partition (a frame split over ranks by
+  // block rows, host/strips.h) img is this rank's strip: the entries, bulk
+  // changes and tail changes of its owned blocks are made here, and the
+  // frame-wide quantities -- the sorted change order, the histograms, the
+  // entropy estimate -- are exchanged or replicated.
   const int ncomp = static_cast<int>(jpg.components.size());
-  const int block_width = img->block_w, block_height = img->block_h;
-  const int num_blocks = block_width * block_height;
+  const int block_width = img->block_w;
+  const int num_blocks = block_width * img->block_h;
+  const int own_lo = part_ ? part_->OwnLo() : 0, own_hi = part_ ? part_->OwnHi() : num_blocks;
+  const int gbase = part_ ? part_->LocalBase() : 0;  // frame index of local block 0
   (void)comp_mask;
-  (void)block_height;
+  auto exchange_failed = [&]() {
+    if (err) *err = "strip exchange failed";
+    return false;
+  };
   std::vector<JpegHistogram> ac_histograms(ncomp);
   int jpg_header_size, dc_size;
   {
@@ -1132,6 +1130,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
     out.app_data = jpg.app_data;
     out.com_data = jpg.com_data;
     img->SaveHeaderToJpegData(saved, &out);
+    if (part_) {
+      out.width = part_->width;
+      out.height = part_->height;
+    }
     jpg_header_size = static_cast<int>(JpegHeaderSize(out, params_.clear_metadata));
     size_t num = saved;
     int idx[3];
@@ -1156,6 +1158,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   std::vector<int> last_indexes(num_blocks, 0);
   const std::vector<float> zero_block_max(num_blocks, 0.0f);
   bool first_up_iter = true;
+  const int own_chunks = (own_hi - own_lo + kOrderChunk - 1) / kOrderChunk;
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early) FlushOutput();  // best_size_ must be current
@@ -1169,12 +1172,11 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const std::vector<float>& bmax = first_up_iter ? zero_block_max : cmp_->block_max_distance();
         cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, 1, 1, bmax,
                                                  &block_weight);
-        // the candidate entries of every block in block order (processor.cc:
-        // 806-829), built in parallel over chunks of blocks: entry counts,
-        // their prefix sums, then each chunk fills its own range
-        const int nchunks = (num_blocks + kOrderChunk - 1) / kOrderChunk;
-        std::vector<size_t> chunk_start(nchunks + 1, 0);
-        std::vector<int> chunk_btc(nchunks, 0);
+        // the candidate entries of every (owned) block in block order
+        // (processor.cc:806-829), built in parallel over chunks of blocks:
+        // entry counts, their prefix sums, then each chunk fills its own range
+        std::vector<size_t> chunk_start(own_chunks + 1, 0);
+        std::vector<int> chunk_btc(own_chunks, 0);
         auto block_entries = [&](int bix) -> int {
           if (block_weight[bix] == 0) return 0;
           const int last_index = last_indexes[bix];
@@ -1182,10 +1184,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           const int num_candidates = offsets[bix + 1] - offset;
           return direction > 0 ? std::max(0, num_candidates - last_index) : last_index;
         };
-        ParallelFor(nchunks, [&](int ch) {
+        ParallelFor(own_chunks, [&](int ch) {
           size_t n = 0;
           int btc = 0;
-          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
             const int e = block_entries(bix);
             n += e;
             btc += e > 0 ? 1 : 0;
@@ -1194,29 +1196,38 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           chunk_btc[ch] = btc;
         });
         blocks_to_change = 0;
-        for (int ch = 0; ch < nchunks; ++ch) {
+        for (int ch = 0; ch < own_chunks; ++ch) {
           chunk_start[ch + 1] += chunk_start[ch];
           blocks_to_change += chunk_btc[ch];
         }
-        global_order.resize(chunk_start[nchunks]);
-        ParallelFor(nchunks, [&](int ch) {
+        global_order.resize(chunk_start[own_chunks]);
+        ParallelFor(own_chunks, [&](int ch) {
           std::pair<int, float>* out = global_order.data() + chunk_start[ch];
-          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
             if (block_weight[bix] == 0) continue;
             const int last_index = last_indexes[bix];
             const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
             const int num_candidates = offsets[bix + 1] - offset;
             const float* errs = cand_err.data() + offset;
             const float max_err = max_block_error[bix];
+            const int g = gbase + bix;
             if (direction > 0) {
               for (int i = last_index; i < num_candidates; ++i)
-                *out++ = std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]);
+                *out++ = std::make_pair(g, (errs[i] - max_err) / block_weight[bix]);
             } else {
               for (int i = last_index - 1; i >= 0; --i)
-                *out++ = std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]);
+                *out++ = std::make_pair(g, (max_err - errs[i]) / block_weight[bix]);
             }
           }
         });
+        if (part_) {
+          // the frame's order: every rank's entries in rank (= block) order;
+          // a rank sends its keys and a count per owned block
+          const auto tx = Clock::now();
+          if (!GatherEntries(&global_order, own_lo, own_hi, gbase, &blocks_to_change))
+            return exchange_failed();
+          res_->detail["strip_entries_s"] += Since(tx);
+        }
         if (!global_order.empty()) break;
       }
       res_->detail["backend_order_s"] += Since(tb);
@@ -1266,17 +1277,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const auto tbk = Clock::now();
         sorter.SetPrefix(bulk);
         bulk_cnt_.assign(num_blocks, 0);
-        for (size_t i = 0; i < bulk; ++i) ++bulk_cnt_[global_order[i].first];
-        const int nchunks = (num_blocks + kOrderChunk - 1) / kOrderChunk;
+        for (size_t i = 0; i < bulk; ++i) {
+          const int b = global_order[i].first - gbase;
+          if (b >= own_lo && b < own_hi) ++bulk_cnt_[b];
+        }
         struct ChunkDelta {
           JpegHistogram h[3];
           std::vector<uint32_t> changed;
         };
-        std::vector<ChunkDelta> deltas(nchunks);
-        ParallelFor(nchunks, [&](int ch) {
+        std::vector<ChunkDelta> deltas(own_chunks);
+        ParallelFor(own_chunks, [&](int ch) {
           ChunkDelta& d = deltas[ch];
           int64_t raw_unused = 0;
-          for (int bix = ch * kOrderChunk; bix < std::min(num_blocks, (ch + 1) * kOrderChunk); ++bix) {
+          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
             const int cnt = bulk_cnt_[bix];
             if (!cnt) continue;
             const int bx = bix % block_width, by = bix / block_width;
@@ -1295,12 +1308,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           }
         });
+        // (symbols only: the last slot is the histogram's fixed sentinel count)
+        std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1), 0);
         for (const ChunkDelta& d : deltas) {
-          // (symbols only: the last slot is the histogram's fixed sentinel count)
           for (int c = 0; c < ncomp && c < 3; ++c)
-            for (int q = 0; q + 1 < JpegHistogram::kSize; ++q) ac_histograms[c].counts[q] += d.h[c].counts[q];
+            for (int q = 0; q + 1 < JpegHistogram::kSize; ++q)
+              hsum[c * (JpegHistogram::kSize - 1) + q] += static_cast<int32_t>(d.h[c].counts[q]);
           img->changed.insert(img->changed.end(), d.changed.begin(), d.changed.end());
         }
+        // (the counts wrap: a chunk's removals are negative deltas)
+        if (part_ && !part_->SumAll(hsum.data(), static_cast<int>(hsum.size()))) return exchange_failed();
+        for (int c = 0; c < ncomp && c < 3; ++c)
+          for (int q = 0; q + 1 < JpegHistogram::kSize; ++q)
+            ac_histograms[c].counts[q] += static_cast<uint32_t>(hsum[c * (JpegHistogram::kSize - 1) + q]);
         refresh_raw();
         changed_coeffs = static_cast<int>(bulk);
         res_->detail["backend_bulk_s"] += Since(tbk);
@@ -1313,60 +1333,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       const size_t n_order = global_order.size();
       double codes_s = 0.0;
       int n_codes = 0;
-      // Prefetch window: when the lazy sort hands out a new sorted chunk, the
-      // chunk's per-block state is touched ahead of the (serial) changes in
-      // three dependent passes -- block bookkeeping, then the candidate byte,
-      // then the coefficient block and its non-zero mask -- so the cache
-      // misses of a chunk overlap instead of chaining.  Values are only
-      // prefetched; the loop below reads them as before.
-      size_t prefetched = bulk;
-      auto prefetch_chunk = [&](size_t lo, size_t hi) {
-        for (size_t j = lo; j < hi; ++j) {
-          const int b = global_order[j].first;
-          __builtin_prefetch(&last_indexes[b]);
-          __builtin_prefetch(&offsets[b]);
-        }
-        for (size_t j = lo; j < hi; ++j) {
-          const int b = global_order[j].first;
-          const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
-          const int ci = off + last_indexes[b] + std::min(direction, 0);
-          if (ci >= 0 && ci < static_cast<int>(cand.size())) __builtin_prefetch(&cand[ci]);
-        }
-        for (size_t j = lo; j < hi; ++j) {
-          const int b = global_order[j].first;
-          const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
-          const int ci = off + last_indexes[b] + std::min(direction, 0);
-          if (ci < 0 || ci >= static_cast<int>(cand.size())) continue;
-          const int c = cand[ci] / kDCTBlockSize;
-          __builtin_prefetch(img->block(c, b), 1);
-          __builtin_prefetch(&acm.nz[static_cast<size_t>(c) * num_blocks + b], 1);
-        }
-      };
       double sort_s = 0.0;
-      for (size_t i = bulk; i < n_order; ++i) {
-        if (i >= sorter.sorted()) {
-          const auto ts = Clock::now();
-          sorter.EnsureSorted(i);
-          sort_s += Since(ts);
-        }
-        if (i >= prefetched) {
-          prefetched = std::max(sorter.sorted(), i + 1);
-          prefetch_chunk(i, std::min(prefetched, n_order));
-        }
-        const int bix = global_order[i].first;
-        const int bx = bix % block_width, by = bix / block_width;
-        const int last_idx = last_indexes[bix];
-        const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
-        const int idx = cand[offset + last_idx + std::min(direction, 0)];
-        const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
-        const int* quant = img->quant[c];
-        const JpegComponent& comp = jpg.components[c];
-        const int jpg_bix = by * comp.width_in_blocks + bx;
-        const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
-        acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
-                   &ac_depths[c * JpegHistogram::kSize], &ac_histograms[c], &raw_bits[c]);
-        img->MarkChanged(c, bix, k);
-        last_indexes[bix] += direction;
+      // one change's bookkeeping after it was applied: the decade's codes,
+      // the estimate and the break test; true: stop after change i
+      auto after_change = [&](size_t i) -> bool {
         val_threshold = global_order[i].second;
         ++changed_coeffs;
         const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
@@ -1378,10 +1348,158 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           codes_s += Since(te);
           ++n_codes;
         }
-        if (!needed) continue;
+        if (!needed) return false;
         est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
-        if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta)
-          break;
+        return changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta;
+      };
+      // the change of the next entry of owned block bix applied to img: its
+      // symbol updates into the frame's histograms, or (log) recorded
+      auto apply = [&](int bix, SymbolLog* log) {
+        const int bx = bix % block_width, by = bix / block_width;
+        const int last_idx = last_indexes[bix];
+        const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+        const int idx = cand[offset + last_idx + std::min(direction, 0)];
+        const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+        const int* quant = img->quant[c];
+        const JpegComponent& comp = jpg.components[c];
+        const int jpg_bix = by * comp.width_in_blocks + bx;
+        const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
+        if (log) {
+          int64_t raw_unused = 0;
+          acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
+                     &ac_depths[c * JpegHistogram::kSize], log, &raw_unused);
+        } else {
+          acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
+                     &ac_depths[c * JpegHistogram::kSize], &ac_histograms[c], &raw_bits[c]);
+        }
+        img->MarkChanged(c, bix, k);
+        last_indexes[bix] += direction;
+      };
+      if (!part_) {
+        // Prefetch window: when the lazy sort hands out a new sorted chunk, the
+        // chunk's per-block state is touched ahead of the (serial) changes in
+        // three dependent passes -- block bookkeeping, then the candidate byte,
+        // then the coefficient block and its non-zero mask -- so the cache
+        // misses of a chunk overlap instead of chaining.  Values are only
+        // prefetched; the loop below reads them as before.
+        size_t prefetched = bulk;
+        auto prefetch_chunk = [&](size_t lo, size_t hi) {
+          for (size_t j = lo; j < hi; ++j) {
+            const int b = global_order[j].first;
+            __builtin_prefetch(&last_indexes[b]);
+            __builtin_prefetch(&offsets[b]);
+          }
+          for (size_t j = lo; j < hi; ++j) {
+            const int b = global_order[j].first;
+            const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
+            const int ci = off + last_indexes[b] + std::min(direction, 0);
+            if (ci >= 0 && ci < static_cast<int>(cand.size())) __builtin_prefetch(&cand[ci]);
+          }
+          for (size_t j = lo; j < hi; ++j) {
+            const int b = global_order[j].first;
+            const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
+            const int ci = off + last_indexes[b] + std::min(direction, 0);
+            if (ci < 0 || ci >= static_cast<int>(cand.size())) continue;
+            const int c = cand[ci] / kDCTBlockSize;
+            __builtin_prefetch(img->block(c, b), 1);
+            __builtin_prefetch(&acm.nz[static_cast<size_t>(c) * num_blocks + b], 1);
+          }
+        };
+        for (size_t i = bulk; i < n_order; ++i) {
+          if (i >= sorter.sorted()) {
+            const auto ts = Clock::now();
+            sorter.EnsureSorted(i);
+            sort_s += Since(ts);
+          }
+          if (i >= prefetched) {
+            prefetched = std::max(sorter.sorted(), i + 1);
+            prefetch_chunk(i, std::min(prefetched, n_order));
+          }
+          apply(global_order[i].first, nullptr);
+          if (after_change(i)) break;
+        }
+      } else {
+        // The tail on a partitioned frame, a window of entries at a time: the
+        // owners apply theirs tentatively and publish the symbol updates,
+        // every rank replays them in order into the frame's histograms and
+        // finds the break; the owners undo what lies past it.
+        struct Undo {
+          size_t i;
+          int bix, c, k;
+          coeff_t old;
+          uint64_t nz;
+        };
+        std::vector<Undo> undo;
+        size_t window = 4096;
+        size_t i = bulk;
+        bool stop = false;
+        while (!stop && i < n_order) {
+          const size_t W = std::min(window, n_order - i);
+          if (i + W > sorter.sorted()) {
+            const auto ts = Clock::now();
+            sorter.EnsureSorted(i + W - 1);
+            sort_s += Since(ts);
+          }
+          std::vector<uint8_t> rec;
+          undo.clear();
+          for (size_t j = i; j < i + W; ++j) {
+            const int bix = global_order[j].first - gbase;
+            if (bix < own_lo || bix >= own_hi) continue;
+            const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+            const int idx = cand[off + last_indexes[bix] + std::min(direction, 0)];
+            const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+            undo.push_back(Undo{j, bix, c, k, img->block(c, bix)[k],
+                                acm.nz[static_cast<size_t>(c) * num_blocks + bix]});
+            SymbolLog log;
+            apply(bix, &log);
+            const uint32_t pos = static_cast<uint32_t>(j - i);
+            rec.insert(rec.end(), reinterpret_cast<const uint8_t*>(&pos),
+                       reinterpret_cast<const uint8_t*>(&pos) + 4);
+            rec.push_back(static_cast<uint8_t>(c));
+            rec.push_back(log.n);
+            for (int e = 0; e < log.n; ++e) {
+              rec.push_back(log.sym[e]);
+              rec.push_back(static_cast<uint8_t>(log.weight[e]));
+            }
+          }
+          const auto tx = Clock::now();
+          std::vector<std::vector<uint8_t>> all;
+          if (!part_->coll->AllGatherV(rec, &all)) return exchange_failed();
+          res_->detail["strip_tail_exchange_s"] += Since(tx);
+          std::vector<const uint8_t*> at(W, nullptr);
+          for (const auto& m : all)
+            for (const uint8_t* p = m.data(); p < m.data() + m.size();) {
+              uint32_t pos;
+              std::memcpy(&pos, p, 4);
+              if (pos >= W) return exchange_failed();
+              at[pos] = p + 4;
+              p += 6 + 2 * p[5];
+            }
+          size_t j = i;
+          for (; j < i + W; ++j) {
+            const uint8_t* r = at[j - i];
+            if (!r) return exchange_failed();
+            const int c = r[0];
+            for (int e = 0; e < r[1]; ++e) {
+              const int sym = r[2 + 2 * e], w = static_cast<int8_t>(r[3 + 2 * e]);
+              ac_histograms[c].Add(sym, w);
+              raw_bits[c] += static_cast<int64_t>(w) * (ac_depths[c * JpegHistogram::kSize + sym] + (sym & 0xf));
+            }
+            if (after_change(j)) {
+              stop = true;
+              break;
+            }
+          }
+          if (stop) {
+            for (auto u = undo.rbegin(); u != undo.rend() && u->i > j; ++u) {
+              img->block(u->c, u->bix)[u->k] = u->old;
+              acm.nz[static_cast<size_t>(u->c) * num_blocks + u->bix] = u->nz;
+              last_indexes[u->bix] -= direction;
+            }
+          }
+          i = stop ? j + 1 : i + W;
+          window *= 2;
+        }
       }
       res_->detail["backend_changes_s"] += Since(tc);
       res_->detail["backend_codes_s"] += codes_s;
@@ -1398,6 +1516,53 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   }
   FlushOutput();
   return true;
+}
+
+// The frame's change entries of one back-end iteration from every rank's
+// owned ones (each rank sends its keys and an entry count per owned block;
+// the pairs are rebuilt in rank order, which is block order).  *entries holds
+// this rank's on entry, the frame's on return; *blocks_to_change becomes the
+// frame's count.
+bool Processor::GatherEntries(std::vector<std::pair<int, float>>* entries, int own_lo, int own_hi,
+                              int gbase, int* blocks_to_change) {
+  const int nown = own_hi - own_lo;
+  std::vector<uint8_t> send(8 + nown + entries->size() * 4, 0);
+  const uint32_t n = static_cast<uint32_t>(entries->size()), btc = static_cast<uint32_t>(*blocks_to_change);
+  std::memcpy(send.data(), &n, 4);
+  std::memcpy(send.data() + 4, &btc, 4);
+  uint8_t* cnt = send.data() + 8;
+  float* keys = reinterpret_cast<float*>(send.data() + 8 + nown);
+  for (size_t i = 0; i < entries->size(); ++i) {
+    ++cnt[(*entries)[i].first - gbase - own_lo];
+    std::memcpy(keys + i, &(*entries)[i].second, 4);
+  }
+  std::vector<std::vector<uint8_t>> all;
+  if (!part_->coll->AllGatherV(send, &all)) return false;
+  size_t total = 0;
+  int frame_btc = 0;
+  for (const auto& m : all) {
+    uint32_t v;
+    std::memcpy(&v, m.data(), 4);
+    total += v;
+    std::memcpy(&v, m.data() + 4, 4);
+    frame_btc += static_cast<int>(v);
+  }
+  entries->resize(total);
+  size_t at = 0;
+  for (int r = 0; r < part_->world; ++r) {
+    const std::vector<uint8_t>& m = all[r];
+    const int b0 = part_->row0[r] * part_->bw, nb = (part_->row0[r + 1] - part_->row0[r]) * part_->bw;
+    const uint8_t* c = m.data() + 8;
+    const uint8_t* k = m.data() + 8 + nb;
+    for (int b = 0; b < nb; ++b)
+      for (int j = 0; j < c[b]; ++j, ++at, k += 4) {
+        float key;
+        std::memcpy(&key, k, 4);
+        (*entries)[at] = std::make_pair(b0 + b, key);
+      }
+  }
+  *blocks_to_change = frame_btc;
+  return at == total;
 }
 
 // RemoveOriginalQuantization, processor.cc:94-107: coefficients times their
@@ -1832,8 +1997,12 @@ void EncodeRGBToJpegData(const uint8_t* rgb, int w, int h, JpegData* jpg) {
 }
 
 int ProcessJpegData(const ProcessParams& params, const JpegData& jpg, Comparator* cmp,
-                    ProcessResult* result, std::string* err) {
-  Processor proc(params, cmp, result);
+                    ProcessResult* result, std::string* err, Partition* part) {
+  if (part && (params.try_420 || params.force_420)) {
+    if (err) *err = "4:2:0 output of a strip-decomposed frame is not supported";
+    return GZ_ERR_UNSUPPORTED;
+  }
+  Processor proc(params, cmp, result, cmp ? part : nullptr);
   return proc.Run(jpg, err);
 }
 

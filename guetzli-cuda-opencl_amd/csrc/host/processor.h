@@ -141,6 +141,20 @@ bool DeviceFetchJpeg(Engine* e, bool kept, const std::string& prologue, size_t s
 // The histogram stage of it alone (for the search back end's size model).
 int DeviceJpegHistograms(Engine* e, const int q[3][kDCTBlockSize], JpegHistogram dc[3],
                          JpegHistogram ac[3], std::string* err);
+// Staged histograms (6 x 256 plain counts, the non-zero chroma count) ->
+// per-component DC / AC histograms as SaveToJpegData stores them; returns
+// the component count (1 when the chroma is all zero).
+int HistogramsFromStage(const uint32_t* hist, uint64_t chroma, JpegHistogram dc[3],
+                        JpegHistogram ac[3]);
+// Headers (*prologue) and Huffman code tables of an image with these
+// histograms (WriteJpeg's table choice, jpeg_data_writer.cc): for the
+// header hdr, or for SaveToJpegData's header of a w x h image with quant q
+// and meta's APPn / COM data.
+bool PrepareScanFor(const JpegData& hdr, bool strip_metadata, int ncomp, JpegHistogram* dc_h,
+                    JpegHistogram* ac_h, std::string* prologue, JpegCodeTables* codes);
+bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
+                 bool strip_metadata, int ncomp, JpegHistogram* dc_h, JpegHistogram* ac_h,
+                 std::string* prologue, JpegCodeTables* codes);
 
 // guetzli::ButteraugliComparator on the HIP engine.
 class HipButteraugliComparator : public Comparator {
@@ -193,6 +207,8 @@ class HipButteraugliComparator : public Comparator {
   // computed on the device (and left resident as the originals).
   bool OriginalJpegData(JpegData* jpg);
   Engine* engine() { return engine_.get(); }
+  // Brings the device copy of the coefficients up to date with img.
+  bool Sync(const CoeffImage& img) { return SyncCoeffs(img); }
   double seconds_compare = 0.0;
   double cpu_compare = 0.0;  // calling thread's CPU seconds in the compares
   double seconds_zeroing = 0.0;
@@ -257,9 +273,13 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
 // The q=1 4:4:4 JPEG model of an RGB image (EncodeRGBToJpeg).
 void EncodeRGBToJpegData(const uint8_t* rgb, int w, int h, JpegData* jpg);
 
+struct Partition;  // host/strips.h
+
 // guetzli::ProcessJpegData (processor.cc:931-1020) with any comparator
-// (nullptr: image too small for Butteraugli).  Returns 0 or a gz_status.
+// (nullptr: image too small for Butteraugli).  With a partition, jpg and
+// the comparator are this rank's strip of a frame split over ranks
+// (host/strips.h).  Returns 0 or a gz_status.
 int ProcessJpegData(const ProcessParams& params, const JpegData& jpg, Comparator* cmp,
-                    ProcessResult* result, std::string* err);
+                    ProcessResult* result, std::string* err, Partition* part = nullptr);
 
 }  // namespace gz

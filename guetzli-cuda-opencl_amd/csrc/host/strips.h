@@ -1,24 +1,35 @@
 // One large frame over several GPUs (BASELINE configs[4]: 8192x8192 q=84 on
-// 4 MI355X): row strips with a halo.
+// 4 MI355X): row strips with a halo, each rank owning the
+// search state of its strip.
 //
-// Every rank runs the same host search loop (guetzli::ProcessJpegData,
-// processor.cc:931-1020) on the whole coefficient image -- its decisions are
-// deterministic, so the replicas agree without being told -- while its GPU
-// evaluates Butteraugli only on the rank's strip of rows plus a halo.  The
-// halo makes the owned rows exact: a strip whose first row is a multiple of
-// 24 (the res grid's 3, the block size 8 and the blur decimations 2/3/4 all
-// divide it) and that extends kStripHalo rows past its owned rows on each
-// side computes, for the owned rows, the distance map, block maxima, mask and
-// per-block zeroing orders of the full image bit for bit (the Butteraugli
-// receptive field is about -60/+66 rows; the strip's own
-// borders fall inside the halo).  Checked on the CPU oracle in
+// Rank r owns block rows [ob0, ob1) and its GPU computes rows [e0, e1) =
+// owned rows plus a kStripHalo-row halo on each side.  The halo makes the
+// owned rows exact: a strip whose first row is a multiple of 24 (the res
+// grid's 3, the block size 8 and the blur decimations 2/3/4 all divide it)
+// and that extends kStripHalo rows past its owned rows computes, for the
+// owned rows, the distance map, block maxima, mask and per-block zeroing
+// orders of the full image bit for bit (the Butteraugli receptive field is
+// about -60/+66 rows).  Checked on the CPU oracle in
 // tests/test_strips.py.
 //
-// The exchanges are the collectives of the path: per Compare an all-gather
-// of the owned block maxima (the distance is their maximum), per
-// SelectFrequencyMasking an all-gather of the owned blocks' zeroing
-// candidates.  Coefficient edits need no exchange: every rank holds the
-// whole image and applies the same edits.
+// Every rank runs the search loop (guetzli::ProcessJpegData, processor.cc:
+// 931-1020) with the same control decisions, but holds and edits only its
+// strip: the back end (processor.cc:723-919) builds the change entries of
+// its owned blocks, applies the changes of its owned blocks and codes its
+// owned MCUs; what the decisions need from the whole frame comes from the
+// exchanges below (the Partition's collectives):
+//   * per Compare: the owned blocks' maxima (the distance is their maximum,
+//     and the block weights of the back end read the neighbours' ones);
+//   * per coded candidate: the owned MCUs' symbol histograms (the Huffman
+//     codes are those of their sum; every rank derives every rank's bit
+//     count from them, so each codes its MCUs at its own bit offset), then
+//     the 0xff counts and the words two ranks' parts share;
+//   * per back-end iteration: the change entries (std::sort's order over the
+//     whole frame is computed on every rank: its ties decide), the bulk
+//     prefix's histogram deltas, and per window of the serial tail the
+//     symbol deltas of the owners' changes;
+//   * before any device work: the owned coefficients changed within
+//     kStripHalo rows of a strip edge, into the neighbours' halos.
 #pragma once
 
 #include <stdint.h>
@@ -53,13 +64,37 @@ class Collectives {
   bool AllGatherV(const std::vector<uint8_t>& send, std::vector<std::vector<uint8_t>>* out);
 };
 
-// guetzli::Comparator for the whole image, backed by a comparator (`inner`)
-// of this rank's computed strip.  `inner` may be null for a rank without
-// rows (it still takes part in every exchange).
-class StripComparator : public Comparator {
+// This rank's share of a frame split by block rows, and the exchanges the
+// search loop makes (ProcessJpegData with a partition; see the top).
+struct Partition {
+  Collectives* coll = nullptr;
+  int world = 1, rank = 0;
+  int width = 0, height = 0;  // the frame
+  int bw = 0, bh = 0;         // its 8x8 blocks
+  int lb0 = 0, lb1 = 0;       // block rows of this rank's image (owned + halo)
+  int ob0 = 0, ob1 = 0;       // owned block rows
+  std::vector<int> row0;      // rank r owns block rows [row0[r], row0[r + 1])
+
+  static Partition Make(const StripLayout& layout, Collectives* coll);
+  int LocalBase() const { return lb0 * bw; }  // frame index of local block 0
+  int OwnLo() const { return (ob0 - lb0) * bw; }
+  int OwnHi() const { return (ob1 - lb0) * bw; }
+  bool OwnsRow(int row) const { return row >= ob0 && row < ob1; }
+  // In-place sums of n values over the ranks (an all-gather, summed in rank
+  // order: integer sums, exact).
+  bool SumAll(int64_t* v, int n);
+};
+
+// guetzli::Comparator for a rank's strip image (block rows [lb0, lb1) of the
+// frame), backed by a comparator of the same strip (`inner`: the HIP one, or
+// any other -- without a device writer the strip is entropy coded on the
+// host).  Every call that reads the image first brings its halo rows up to
+// date with the neighbours' owned changes (a collective); the search loop
+// itself only edits owned blocks.
+class PartitionComparator : public Comparator {
  public:
-  StripComparator(const StripLayout& layout, std::unique_ptr<Comparator> inner, Collectives* coll,
-                  float target);
+  PartitionComparator(Partition* part, std::unique_ptr<Comparator> inner, float target);
+  ~PartitionComparator() override;
   bool Compare(const CoeffImage& img) override;
   bool StartBlockComparisons() override;
   void FinishBlockComparisons() override;
@@ -71,6 +106,14 @@ class StripComparator : public Comparator {
                               std::vector<float>* err) override;
   bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
                             bool need_host = true) override;
+  bool HasDeviceWriter() const override { return true; }
+  bool DeviceEncodeAndCompare(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                              size_t* size) override;
+  bool DeviceEncodeOriginalAndCompare(const CoeffImage& img, const JpegData& jpg_in,
+                                      bool strip_metadata, size_t* size, bool* used) override;
+  void DeviceKeepEncoded() override;
+  bool DeviceFetchKept(std::string* out) override;
+  int DeviceHistograms(const CoeffImage& img, JpegHistogram dc[3], JpegHistogram ac[3]) override;
   double ScoreOutputSize(int size) const override { return ScoreJPEG(distance_, size, target_); }
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }
   float distmap_aggregate() const override { return distance_; }
@@ -84,34 +127,46 @@ class StripComparator : public Comparator {
   const std::string& error() const override { return err_; }
   Comparator* inner() { return inner_.get(); }
   double seconds_exchange = 0.0;
+  double seconds_halo = 0.0;
+
+  // The part of the scan this rank codes (frame-wide bit offset, bits, the
+  // words shared with its neighbours) -- Engine::ScanPart's fields.
+  struct Part {
+    uint64_t base = 0, bits = 0, ff = 0;
+    uint32_t first_word = 0, last_word = 0;
+    bool first_shared = false, last_open = false;
+  };
+  class Coder;  // the strip's entropy coder (device or host)
 
  private:
-  // Fails on every rank if any rank's status word is non-zero.
-  bool CheckStatus(const std::vector<uint32_t>& status, const std::string& local);
   bool Fail(const std::string& what);
-  bool Sync(const CoeffImage& img);  // the strip's coefficients <- the whole image's
-  int rank_blocks() const { return (ob1_ - ob0_) * bw_; }
+  // An exchange with a status word: fails on every rank if any rank failed.
+  bool Exchange(bool ok, const std::string& local_err, const std::vector<uint8_t>& send,
+                std::vector<std::vector<uint8_t>>* all);
+  bool Agree(bool ok, const std::string& local_err);
+  bool SyncHalo(const CoeffImage& img);
+  // Codes img (headers: SaveToJpegData's, or *hdr's), overlapped with the
+  // Compare of img; *size the whole file's size.
+  bool CodeAndCompare(const CoeffImage& img, const JpegData& meta, const JpegData* hdr,
+                      bool strip_metadata, size_t* size);
 
-  StripLayout layout_;
+  Partition* part_;
   std::unique_ptr<Comparator> inner_;
-  Collectives* coll_;
+  std::unique_ptr<Coder> coder_;
   float target_;
-  int rank_ = 0, bw_ = 0, blocks_ = 0;
-  int lb0_ = 0, lb1_ = 0;  // computed block rows
-  int ob0_ = 0, ob1_ = 0;  // owned block rows
-  int max_owned_ = 0;      // owned blocks of the largest strip
-  CoeffImage local_;       // the computed strip's coefficients
-  JpegData local_orig_;    // and its q=1 originals
-  CoeffCursor synced_;     // what local_ reflects of the whole image
-  std::vector<coeff_t> orig_;  // q=1 originals of the whole image
-  std::vector<float> block_max_;
+  int local_blocks_ = 0;
+  CoeffCursor halo_;            // the image journal position already exchanged
+  std::vector<float> block_max_;  // local blocks
   float distance_ = 0.0f;
+  std::string cur_prologue_, kept_prologue_;
+  size_t cur_size_ = 0, kept_size_ = 0;
   std::string err_;
 };
 
-// guetzli::Process for one frame whose Butteraugli work is split over the
-// ranks of `coll` (one GPU each, `device` on this rank): every rank passes the
-// whole RGB frame and gets the same JPEG bytes.  Returns 0 or a gz_status.
+// guetzli::Process for one frame whose work is split over the ranks of
+// `coll` (one GPU each, `device` on this rank): every rank passes the whole
+// RGB frame and gets the same JPEG bytes.  Every rank must own rows (height
+// >= 24 * world).  Returns 0 or a gz_status.
 int ProcessStrips(int device, const ProcessParams& params, const uint8_t* rgb, int w, int h,
                   Collectives* coll, ProcessResult* result, std::string* err);
 

@@ -447,14 +447,20 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jwords_[1]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jinfo_), 16);
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 16, hipHostMallocCoherent) != hipSuccess)
+  const size_t code_groups = (static_cast<size_t>(e->nb_) + kCodeMcus - 1) / kCodeMcus;
+  // 0xff counters | arrival counters | status words | shared words
+  const size_t jctl_bytes = kCodeFfCopies * 8 + (1 + code_groups / 64 + 2) * 8 + code_groups * 8 +
+                            code_groups * 16;
+  alloc(reinterpret_cast<void**>(&e->d_jctl_), jctl_bytes);
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 64, hipHostMallocCoherent) != hipSuccess)
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_jhist_), e->h_jhist_, 0) != hipSuccess)
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodesPacked)) != hipSuccess)
     ok = false;
   if (ok && (hipMemsetAsync(e->d_jhist_, 0, kJHistDeviceBytes, s) != hipSuccess ||
-             hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess))
+             hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess ||
+             hipMemsetAsync(e->d_jctl_, 0, jctl_bytes, s) != hipSuccess))
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
@@ -558,7 +564,7 @@ Engine::~Engine() {
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
-                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_zero_nnz_,
+                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_jctl_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -1234,9 +1240,12 @@ bool Engine::JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz) 
   return JpegStageEnqueue(q) && JpegStageWait(hist, chroma_nz);
 }
 
-bool Engine::JpegStageEnqueue(const int q[3][64]) {
+bool Engine::JpegStageEnqueue(const int q[3][64]) { return JpegStageEnqueueRange(q, 0, nb_); }
+
+bool Engine::JpegStageEnqueueRange(const int q[3][64], int m0, int m1) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  if (m0 < 0 || m1 > nb_ || m1 <= m0) return Fail("JpegStage block range", 0);
   if (!stage_event_) {
     hipEvent_t ev;
     GZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1247,8 +1256,8 @@ bool Engine::JpegStageEnqueue(const int q[3][64]) {
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
   // (the device counts are zero: cleared at creation, and by the last
   // workgroup of every stage after it has published them to h_jhist_)
-  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * nb_ + kStageBlocks - 1) / kStageBlocks, 1024, 0, s>>>(
-      d_cur_, qf, nb_, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
+  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, 1024, 0, s>>>(
+      d_cur_, qf, nb_, m0, m1, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;
 }
@@ -1272,9 +1281,15 @@ bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, u
 // (the caller has synchronised since the previous scan: the pinned code
 // staging is free)
 bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
+  return JpegScanEnqueueRange(ncomp, codes, 0, nb_, 0, true);
+}
+
+bool Engine::JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0, int m1, uint64_t base,
+                                  bool pad_end) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
+  if (m0 < 0 || m1 > nb_ || m1 <= m0) return Fail("JpegScan block range", 0);
   for (int c = 0; c < 3; ++c)
     for (int i = 0; i < 256; ++i) {
       h_jcodes_->e[c][i] = (static_cast<uint32_t>(codes.dc_len[c][i]) << 16) | codes.dc_code[c][i];
@@ -1282,24 +1297,64 @@ bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
     }
   GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodesPacked), hipMemcpyHostToDevice, s));
   const JpegCodesPacked* dc = static_cast<const JpegCodesPacked*>(d_jcodes_);
+  // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any
+  // scan of these MCUs, plus the word of an unaligned start)
   uint32_t* words = d_jwords_[jslot_];
-  const unsigned mcu_groups = static_cast<unsigned>((nb_ + 3) / 4);
-  GZ_TIMED("jpeg_bits", k_jpeg_bits<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitlen_, d_scan_sums_));
-  if (!ScanCounts(d_jbitlen_, nb_, d_jbitoff_, "jpeg_scan", d_scan_sums_, 4, words, d_jinfo_)) return false;
-  // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any scan)
-  GZ_TIMED("jpeg_emit", (k_jpeg_emit<<<mcu_groups, 256, 0, s>>>(d_jzz_, nb_, ncomp, dc, d_jbitoff_, words),
-                         k_jpeg_pad_count<<<64, 256, 0, s>>>(d_jbitoff_ + nb_, words, d_jinfo_,
-                                                              m_jhist_ + 6 * 256 + 2)));
-  // (0xff count, bit total) reach h_jhist_[1538..1539] from the last workgroup
+  const int groups = (m1 - m0 + kCodeMcus - 1) / kCodeMcus;
+  // launch counter: tags the status words (low 14 bits) and the published
+  // shared words (all 32; 0 is the zeroed arrays' tag, never used)
+  if (++jepoch_ == 0) jepoch_ = 1;
+  const size_t max_groups = (static_cast<size_t>(nb_) + kCodeMcus - 1) / kCodeMcus;
+  unsigned long long* ffc = reinterpret_cast<unsigned long long*>(d_jctl_);
+  uint32_t* arr = d_jctl_ + 2 * kCodeFfCopies;
+  uint64_t* status = reinterpret_cast<uint64_t*>(arr) + 1 + max_groups / 64 + 2;
+  uint64_t* side = status + max_groups;
+  GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_jzz_, nb_, m0, m1, ncomp, dc,
+                                                            static_cast<unsigned long long>(base),
+                                                            pad_end ? 1 : 0, words, ffc, arr, status, side,
+                                                            jepoch_, m_jhist_ + 6 * 256 + 2));
+  jpart_[jslot_].base = base;
+  // (0xff count, bit total, shared words) reach h_jhist_[1538..1543] from
+  // the last workgroup to finish
+  return true;
+}
+
+bool Engine::JpegScanFinishPart(ScanPart* part) {
+  ScanPart& p = jpart_[jslot_];
+  const uint32_t* h = h_jhist_ + 6 * 256 + 2;
+  p.ff = h[0];
+  p.bits = static_cast<uint64_t>(h[1]) | (static_cast<uint64_t>(h[2]) << 32);
+  p.first_word = h[3];
+  p.last_word = h[4];
+  p.first_shared = (h[5] & 1) != 0;
+  p.last_open = (h[5] & 2) != 0;
+  if (h[5] & 4) return Fail("JpegScan: a part under one word", 0);
+  if ((p.base % 32 + p.bits + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
+  jnbits_[jslot_] = p.bits;
+  if (part) *part = p;
   return true;
 }
 
 bool Engine::JpegScanFinish(uint64_t* nbits, uint64_t* ff) {
-  const uint64_t total = static_cast<uint32_t>(h_jhist_[6 * 256 + 3]);
-  if ((total + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
-  jnbits_[jslot_] = total;
-  *nbits = total;
-  *ff = h_jhist_[6 * 256 + 2];
+  ScanPart p;
+  if (!JpegScanFinishPart(&p)) return false;
+  *nbits = p.bits;
+  *ff = p.ff;
+  return true;
+}
+
+bool Engine::JpegFetchPart(bool kept, std::vector<uint32_t>* words, ScanPart* part) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  const int slot = kept ? jslot_ ^ 1 : jslot_;
+  const ScanPart& p = jpart_[slot];
+  const size_t nw = static_cast<size_t>((p.base % 32 + p.bits + 31) / 32);
+  words->assign(nw, 0u);
+  if (nw) GZ_HIP(hipMemcpyAsync(words->data(), d_jwords_[slot], nw * 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  if (p.first_shared && nw) (*words)[0] = 0u;            // (not stored by the coder)
+  if (p.last_open && nw) (*words)[nw - 1] = 0u;
+  *part = p;
   return true;
 }
 

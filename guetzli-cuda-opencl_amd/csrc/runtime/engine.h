@@ -162,6 +162,27 @@ class Engine {
   bool Sync();
   void CompareFinish(float* distance, float* block_max);
   bool JpegScanFinish(uint64_t* nbits, uint64_t* ff);
+
+  // The coder over a part of the scan (a frame split over ranks by block
+  // rows): the MCUs [m0, m1) (4:4:4, one block per component), their DC
+  // predicted from block m0 - 1, their bits starting at bit `base` of the
+  // whole stream; pad_end for the stream's last part.  The words this part
+  // shares with its neighbours (first_word when base is not a multiple of
+  // 32, last_word when the end is neither padded nor word-aligned) are not
+  // stored: they come back here, in memory byte order, for the ranks to
+  // combine; ff counts the 0xff bytes of the words the part stores.
+  struct ScanPart {
+    uint64_t base = 0, bits = 0, ff = 0;
+    uint32_t first_word = 0, last_word = 0;
+    bool first_shared = false, last_open = false;
+  };
+  bool JpegStageEnqueueRange(const int q[3][64], int m0, int m1);
+  bool JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0, int m1, uint64_t base,
+                            bool pad_end);
+  bool JpegScanFinishPart(ScanPart* part);
+  // The stored words of a slot's part (memory byte order; words[0] is the
+  // stream's word base >> 5, the shared ones zero) and its ScanPart.
+  bool JpegFetchPart(bool kept, std::vector<uint32_t>* words, ScanPart* part);
   bool ScanCounts(const int* counts, int n, int* offsets, const char* name,
                   const int* group_sums = nullptr, int per = 0, uint32_t* zero_words = nullptr,
                   int* info = nullptr);
@@ -246,8 +267,11 @@ class Engine {
   int* d_jbitoff_ = nullptr;       //   [blocks + 1]
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
+  ScanPart jpart_[2];
   int jslot_ = 0;                  // current slot (kept = jslot_ ^ 1)
   int* d_jinfo_ = nullptr;         //   0xff count, bit total, done counter
+  uint32_t* d_jctl_ = nullptr;     //   k_jpeg_code: 0xff counters | arrivals | status | shared words
+  uint32_t jepoch_ = 0;            //   launches so far (status tags)
   size_t jwords_cap_ = 0;
   uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + (0xff count, total bits),
   uint32_t* m_jhist_ = nullptr;    //   written by the kernels through this mapped address

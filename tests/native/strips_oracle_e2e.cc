@@ -1,7 +1,8 @@
 // CPU end-to-end check of the row-strip decomposition (host/strips.h): WORLD
-// ranks run as threads, each with the product's StripComparator over a
-// CPU-oracle comparator of its strip (rows + halo) and an in-process
-// all-gather; every rank must produce the single-comparator bytes.  Test
+// ranks run as threads, each with the product's partitioned search loop and
+// PartitionComparator over a CPU-oracle comparator of its strip (rows +
+// halo; the strip's entropy coding then runs on the host) and an in-process
+// all-gather; every rank must produce the reference bytes.  Test
 // infrastructure only.
 //
 //   strips_oracle_e2e RGB W H QUALITY WORLD OUT.jpg [FAIL_RANK compare|zeroing N]
@@ -93,19 +94,18 @@ int main(int argc, char** argv) {
   for (int r = 0; r < world; ++r) {
     ranks.emplace_back([&, r] {
       ThreadCollectives coll(&x, r);
+      // this rank's strip (owned rows + halo): its q=1 coefficients, an
+      // oracle comparator of its rows, the product's partitioned search
+      const int e0 = L.e0[r], hs = L.e1[r] - L.e0[r];
+      const uint8_t* srgb = rgb.data() + static_cast<size_t>(3) * w * e0;
       gz::JpegData jpg;
-      gz::EncodeRGBToJpegData(rgb.data(), w, h, &jpg);
-      std::unique_ptr<gz::Comparator> inner;
-      if (L.y1[r] > L.y0[r]) {
-        auto* oc = new gz_test::OracleComparator(w, L.e1[r] - L.e0[r],
-                                                 rgb.data() + static_cast<size_t>(3) * w * L.e0[r],
-                                                 params.butteraugli_target);
-        if (r == fail_rank) (fail_kind == "compare" ? oc->fail_compare_at : oc->fail_zeroing_at) = fail_at;
-        inner.reset(oc);
-      }
-      gz::StripComparator cmp(L, std::move(inner), &coll, params.butteraugli_target);
+      gz::EncodeRGBToJpegData(srgb, w, hs, &jpg);
+      auto* oc = new gz_test::OracleComparator(w, hs, srgb, params.butteraugli_target);
+      if (r == fail_rank) (fail_kind == "compare" ? oc->fail_compare_at : oc->fail_zeroing_at) = fail_at;
+      gz::Partition part = gz::Partition::Make(L, &coll);
+      gz::PartitionComparator cmp(&part, std::unique_ptr<gz::Comparator>(oc), params.butteraugli_target);
       gz::ProcessResult res;
-      rc[r] = gz::ProcessJpegData(params, jpg, &cmp, &res, &errs[r]);
+      rc[r] = gz::ProcessJpegData(params, jpg, &cmp, &res, &errs[r], &part);
       out[r] = res.jpeg;
       iters[r] = res.iterations;
     });
