@@ -1220,7 +1220,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           }
         });
-        if (part_) {
+        if (part_ && part_->world > 1) {
           // the frame's order: every rank's entries in rank (= block) order;
           // a rank sends its keys and a count per owned block
           const auto tx = Clock::now();
@@ -1375,7 +1375,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         img->MarkChanged(c, bix, k);
         last_indexes[bix] += direction;
       };
-      if (!part_) {
+      if (!part_ || part_->world == 1) {
         // Prefetch window: when the lazy sort hands out a new sorted chunk, the
         // chunk's per-block state is touched ahead of the (serial) changes in
         // three dependent passes -- block bookkeeping, then the candidate byte,

@@ -383,6 +383,11 @@ bool PartitionComparator::Fail(const std::string& what) {
 bool PartitionComparator::Exchange(bool ok, const std::string& local_err,
                                    const std::vector<uint8_t>& send,
                                    std::vector<std::vector<uint8_t>>* all) {
+  if (part_->world == 1) {
+    if (!ok) return Fail(local_err);
+    all->assign(1, send);
+    return true;
+  }
   std::vector<uint8_t> msg;
   Put(&msg, static_cast<uint32_t>(ok ? 0 : 1));
   if (ok) msg.insert(msg.end(), send.begin(), send.end());
@@ -408,6 +413,7 @@ bool PartitionComparator::Exchange(bool ok, const std::string& local_err,
 // the search image (whose halo rows the search loop never edits) and its
 // journal, so every mirror of it (the device copy) follows.
 bool PartitionComparator::SyncHalo(const CoeffImage& img) {
+  if (part_->world == 1) return true;  // (no halo rows)
   const auto t0 = Clock::now();
   const Partition& P = *part_;
   const int halo_rows = kStripHalo / 8;
@@ -483,6 +489,7 @@ bool PartitionComparator::Compare(const CoeffImage& img) {
 // A local step's outcome agreed on by every rank (one small all-gather), so
 // that a failing rank does not leave the others in the next exchange.
 bool PartitionComparator::Agree(bool ok, const std::string& local_err) {
+  if (part_->world == 1) return ok || Fail(local_err);
   const uint32_t mine = ok ? 0u : 1u;
   std::vector<uint32_t> st(part_->world);
   if (!part_->coll->AllGather(&mine, sizeof(mine), st.data()))

@@ -438,15 +438,13 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   alloc(reinterpret_cast<void**>(&e->d_jzz_), nc * sizeof(int16_t));
   alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
-  alloc(reinterpret_cast<void**>(&e->d_jhist_), kJHistDeviceBytes);
+  const size_t stage_groups = (3 * static_cast<size_t>(e->nb_) + kStageBlocks - 1) / kStageBlocks;
+  alloc(reinterpret_cast<void**>(&e->d_jhist_), jhist_device_bytes(stage_groups));
   alloc(&e->d_jcodes_, sizeof(JpegCodesPacked));
-  alloc(reinterpret_cast<void**>(&e->d_jbitlen_), static_cast<size_t>(e->nb_) * 4);
-  alloc(reinterpret_cast<void**>(&e->d_jbitoff_), static_cast<size_t>(e->nb_ + 1) * 4);
   // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
   e->jwords_cap_ = static_cast<size_t>(e->nb_) * 160 + 16;
   alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jwords_[1]), e->jwords_cap_ * 4);
-  alloc(reinterpret_cast<void**>(&e->d_jinfo_), 16);
   const size_t code_groups = (static_cast<size_t>(e->nb_) + kCodeMcus - 1) / kCodeMcus;
   // 0xff counters | arrival counters | status words | shared words
   const size_t jctl_bytes = kCodeFfCopies * 8 + (1 + code_groups / 64 + 2) * 8 + code_groups * 8 +
@@ -458,8 +456,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodesPacked)) != hipSuccess)
     ok = false;
-  if (ok && (hipMemsetAsync(e->d_jhist_, 0, kJHistDeviceBytes, s) != hipSuccess ||
-             hipMemsetAsync(e->d_jinfo_, 0, 16, s) != hipSuccess ||
+  if (ok && (hipMemsetAsync(e->d_jhist_, 0, jhist_device_bytes(stage_groups), s) != hipSuccess ||
              hipMemsetAsync(e->d_jctl_, 0, jctl_bytes, s) != hipSuccess))
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
@@ -564,7 +561,7 @@ Engine::~Engine() {
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
-                  d_jmask_, d_jhist_, d_jcodes_, d_jbitlen_, d_jbitoff_, d_jwords_[0], d_jwords_[1], d_jinfo_, d_jctl_, d_zero_nnz_,
+                  d_jmask_, d_jhist_, d_jcodes_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -1075,18 +1072,12 @@ static size_t BzLdsPad() {
 }
 
 // offsets[0..n] = exclusive prefix sums of the device counts[0..n), on the stream.
-bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name,
-                        const int* group_sums, int per, uint32_t* zero_words, int* info) {
+bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (n > nb_) return Fail("ScanCounts size", 0);
   const unsigned chunks = static_cast<unsigned>((n + kScanChunk - 1) / kScanChunk);
-  if (group_sums) {
-    GZ_TIMED(name, k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, group_sums, per, offsets, zero_words, info));
-  } else {
-    GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
-                    k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, kScanChunk, offsets,
-                                                         zero_words, info)));
-  }
+  GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
+                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets)));
   return true;
 }
 

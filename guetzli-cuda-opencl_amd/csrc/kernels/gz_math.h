@@ -518,21 +518,32 @@ __device__ __forceinline__ void real_fft8(const T* in, T* re, T* im, T sqrt_half
   fft_reorder8(re, im);
 }
 
-// True in every thread of the last workgroup to reach this point (all
-// threads of every workgroup must call it); *done counts arrivals and is
-// reset to 0 by the last one.  Only for data that every workgroup updates
-// and the last one reads with device-scope atomics (coherent across the
-// XCDs' L2s): the barrier waits for this workgroup's atomics to complete
-// before the arrival is counted.  No device-scope fence -- on gfx950 that
-// writes back the XCD's L2, which costs more than the whole kernel.
-__device__ __forceinline__ bool last_block_done(uint32_t* done) {
+// True in every thread of the last workgroup of the launch to reach this
+// point (every thread of every workgroup must call it).  Arrivals count in
+// two levels -- workgroup t into arr[1 + t / 64], the last of each 64 into
+// arr[0] -- and every counter is reset by its last arrival: same-address
+// device atomics serialise, so one counter would take one atomic per
+// workgroup in turn.  arr: 1 + ceil(groups / 64) counters, zero on entry.
+// Only for data that every workgroup updates and the last one reads with
+// device-scope atomics (coherent across the XCDs' L2s): the barrier waits
+// for this workgroup's atomics to complete before the arrival is counted.
+// No device-scope fence -- on gfx950 that writes back the XCD's L2, which
+// costs more than the whole kernel.
+__device__ __forceinline__ bool last_arrival(uint32_t* arr, int t, int groups) {
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics acknowledged
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t prev = atomicAdd(done, 1u);
-    const bool last = prev == gridDim.x * gridDim.y * gridDim.z - 1;
-    if (last) atomicExch(done, 0u);
+    const int grp = t >> 6, ngrp = (groups + 63) >> 6;
+    const uint32_t gsize = static_cast<uint32_t>(min(64, groups - (grp << 6)));
+    int last = 0;
+    if (atomicAdd(&arr[1 + grp], 1u) == gsize - 1) {
+      atomicExch(&arr[1 + grp], 0u);
+      if (atomicAdd(&arr[0], 1u) == static_cast<uint32_t>(ngrp - 1)) {
+        atomicExch(&arr[0], 0u);
+        last = 1;
+      }
+    }
     s_last = last;
   }
   __syncthreads();

@@ -183,9 +183,8 @@ class Engine {
   // The stored words of a slot's part (memory byte order; words[0] is the
   // stream's word base >> 5, the shared ones zero) and its ScanPart.
   bool JpegFetchPart(bool kept, std::vector<uint32_t>* words, ScanPart* part);
-  bool ScanCounts(const int* counts, int n, int* offsets, const char* name,
-                  const int* group_sums = nullptr, int per = 0, uint32_t* zero_words = nullptr,
-                  int* info = nullptr);
+  // offsets[i] = counts[0] + ... + counts[i - 1] on the device (n + 1 entries)
+  bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
   bool OrderBlocks(int comp_mask);
 
   const std::string& error() const { return err_; }
@@ -263,13 +262,10 @@ class Engine {
   uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
   uint32_t* d_jhist_ = nullptr;    //   kJHistCopies x 6 x 256 counts + chroma non-zeros (u64) + done counter
   void* d_jcodes_ = nullptr;       //   JpegCodesPacked
-  int* d_jbitlen_ = nullptr;       //   [blocks]
-  int* d_jbitoff_ = nullptr;       //   [blocks + 1]
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
   ScanPart jpart_[2];
   int jslot_ = 0;                  // current slot (kept = jslot_ ^ 1)
-  int* d_jinfo_ = nullptr;         //   0xff count, bit total, done counter
   uint32_t* d_jctl_ = nullptr;     //   k_jpeg_code: 0xff counters | arrivals | status | shared words
   uint32_t jepoch_ = 0;            //   launches so far (status tags)
   size_t jwords_cap_ = 0;

@@ -412,15 +412,21 @@ def process_device(rgb_dev_ptr, width, height, params=None, device=0, return_sta
 class Collectives:
     """The exchange of a multi-rank encode (gz_collectives): an equal-size
     all-gather of byte blocks.  `allgather(data: bytes) -> bytes` must return
-    every rank's block concatenated in rank order.  Keeps the ctypes callback
-    alive for as long as the object lives."""
+    every rank's block concatenated in rank order; or, without copies,
+    `allgather_into(send_ptr, nbytes, recv_ptr)` gathers nbytes from send_ptr
+    of every rank into recv_ptr (world * nbytes, rank order).  Keeps the
+    ctypes callback alive for as long as the object lives."""
 
-    def __init__(self, rank, world, allgather):
+    def __init__(self, rank, world, allgather=None, allgather_into=None):
         self.rank, self.world = rank, world
         self._fn = allgather
+        self._into = allgather_into
 
         def cb(_ctx, send, nbytes, recv):
             try:
+                if self._into is not None:
+                    self._into(send or 0, nbytes, recv or 0)
+                    return 0
                 data = ctypes.string_at(send, nbytes) if nbytes else b""
                 out = self._fn(data)
                 if len(out) != nbytes * self.world:
@@ -438,23 +444,29 @@ class Collectives:
     def from_torch(cls, dist, device="cpu"):
         """Bound to torch.distributed: all_gather_into_tensor of uint8 blocks on
         `device` ("cuda:N" for RCCL over xGMI with the nccl backend, "cpu" for
-        gloo)."""
+        gloo).  The library's buffers are wrapped, not copied: on the CPU the
+        collective reads and writes them in place, on a GPU one H2D copy of
+        the block and one D2H copy of the result."""
         import torch
 
         world, rank = dist.get_world_size(), dist.get_rank()
 
-        def allgather(data):
-            n = len(data)
-            src = torch.zeros(max(n, 1), dtype=torch.uint8)
-            if n:
-                src[:n] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
-            src = src.to(device)
-            dst = torch.empty(world * src.numel(), dtype=torch.uint8, device=device)
-            dist.all_gather_into_tensor(dst, src)
-            blocks = dst.view(world, -1)[:, :n].cpu().numpy()
-            return blocks.tobytes()
+        def wrap(ptr, n):
+            return torch.frombuffer((ctypes.c_uint8 * n).from_address(ptr), dtype=torch.uint8)
 
-        return cls(rank, world, allgather)
+        def allgather_into(send, n, recv):
+            if n == 0:
+                return
+            src, dst = wrap(send, n), wrap(recv, n * world)
+            if str(device) == "cpu":
+                dist.all_gather(list(dst.view(world, n).unbind(0)), src)
+            else:
+                d_src = src.to(device, non_blocking=False)
+                d_dst = torch.empty(world * n, dtype=torch.uint8, device=device)
+                dist.all_gather_into_tensor(d_dst, d_src)
+                dst.copy_(d_dst)
+
+        return cls(rank, world, allgather_into=allgather_into)
 
     def selftest(self):
         _check(lib().gz_collectives_selftest(ctypes.byref(self._c)), "collectives_selftest")

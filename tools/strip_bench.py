@@ -22,6 +22,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
 
 
+def _thread_cpu():
+    """{tid: (cpu seconds, name)} of this process's threads."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            st = open("/proc/self/task/%s/stat" % tid).read()
+            f = st[st.rindex(")") + 2:].split()
+            out[tid] = ((int(f[11]) + int(f[12])) / tick, st[st.index("(") + 1:st.rindex(")")])
+        except (OSError, ValueError):
+            pass
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--width", type=int, default=8192)
@@ -31,6 +45,10 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--warmup", type=int, default=0,
                     help="untimed encodes of the frame first (engine creation, first-touch)")
+    ap.add_argument("--backend", default="nccl",
+                    help="nccl (RCCL over xGMI, one GPU per rank) or gloo (host exchange)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on device 0 (rehearsal of the split on one GPU; gloo)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -38,11 +56,17 @@ def main():
     import torch
     import guetzli_amd as gz
     dist = None
+    if args.one_device:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        coll = gz.Collectives.from_torch(dist, "cuda:%d" % local)
+        if args.backend == "gloo":
+            dist.init_process_group("gloo")
+            coll = gz.Collectives.from_torch(dist, "cpu")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            coll = gz.Collectives.from_torch(dist, "cuda:%d" % local)
     else:
         coll = gz.Collectives(0, 1, lambda b: b)
     w, h = args.width, args.height
@@ -53,9 +77,27 @@ def main():
         del process_strips_once
     if dist is not None:
         dist.barrier()
+    import resource
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    th0 = _thread_cpu()
     t0 = time.perf_counter()
     data, st = gz.process_strips(rgb, w, h, coll, params, device=local, return_stats=True)
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    th1 = _thread_cpu()
+    threads = {}
+    for k, (c, n) in th1.items():
+        threads[n] = threads.get(n, 0.0) + c - th0.get(k, (0.0, n))[0]
+    detail = gz.last_process_detail()
+    host_cpu = [cpu]
+    if dist is not None:
+        c = torch.tensor([cpu] * world, dtype=torch.float64)
+        if args.backend != "gloo":
+            c = c.to("cuda:%d" % local)
+        cs = [torch.zeros_like(c[:1]) for _ in range(world)]
+        dist.all_gather(cs, c[:1])
+        host_cpu = [float(x.item()) for x in cs]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -69,12 +111,23 @@ def main():
                "seconds_compare", "seconds_zeroing", "seconds_write", "seconds_quantize",
                "seconds_backend", "seconds_setup")},
            "strip": gz.strip_layout(w, h, world, rank), "warmup": args.warmup,
-           "detail": gz.last_process_detail()}
-    if args.check and world == 1:
+           "host_cpu_seconds_per_rank": [round(x, 3) for x in host_cpu],
+           "rank0_thread_cpu_seconds": {n: round(c, 3) for n, c in
+                                        sorted(threads.items(), key=lambda x: -x[1]) if c > 0.01},
+           "detail": detail}
+    if args.check and rank == 0:
+        # the single-engine path on this rank's GPU (the others wait)
+        ref = gz.process(rgb, w, h, params, device=local)  # (warm: engine pooled)
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t1 = time.perf_counter()
         ref = gz.process(rgb, w, h, params, device=local)
         out["single_engine_seconds"] = round(time.perf_counter() - t1, 3)
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        out["single_engine_host_cpu_seconds"] = round(
+            (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime), 3)
         out["single_engine_identical"] = ref == data
+    if dist is not None:
+        dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
