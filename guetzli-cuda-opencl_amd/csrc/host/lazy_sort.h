@@ -13,12 +13,22 @@
 // element across a leaf range — it equals a stable insertion sort of each
 // leaf.  Refining leftmost-first and finishing leaves as they are reached
 // therefore yields exactly std::sort's permutation, one prefix at a time.
+//
+// Large ranges are partitioned on the host pool (ParallelPartition): the
+// unguarded Hoare partition is a function of two position lists -- the
+// left scan's stops L (keys >= pivot, ascending) and the right scan's R
+// (keys <= pivot, descending) -- so counting, listing, a binary search for
+// the crossing and the swaps all run in parallel and give the same
+// permutation and cut as the sequential loop.
 #pragma once
 
 #include <stddef.h>
 
+#include <algorithm>
 #include <utility>
 #include <vector>
+
+#include "host/thread_pool.h"
 
 namespace gz {
 
@@ -64,9 +74,7 @@ class LazyStdSort {
         HeapSort(f, l);
         done_ = r.hi;
       } else {
-        Elem* mid = f + (l - f) / 2;
-        MoveMedianToFirst(f, f + 1, mid, l - 1);
-        const size_t cut = static_cast<size_t>(UnguardedPartition(f + 1, l, f) - a_);
+        const size_t cut = Cut(f, l);
         pending_.push_back(Range{cut, r.hi, r.depth - 1});
         pending_.push_back(Range{r.lo, cut, r.depth - 1});
       }
@@ -88,9 +96,7 @@ class LazyStdSort {
         HeapSort(f, l);
         done_ = r.hi;
       } else {
-        Elem* mid = f + (l - f) / 2;
-        MoveMedianToFirst(f, f + 1, mid, l - 1);
-        const size_t cut = static_cast<size_t>(UnguardedPartition(f + 1, l, f) - a_);
+        const size_t cut = Cut(f, l);
         pending_.push_back(Range{cut, r.hi, r.depth - 1});
         pending_.push_back(Range{r.lo, cut, r.depth - 1});
       }
@@ -99,10 +105,77 @@ class LazyStdSort {
 
  private:
   static constexpr size_t kThreshold = 16;
+  static constexpr size_t kParallelMin = size_t{1} << 16;  // ranges partitioned on the pool
   struct Range {
     size_t lo, hi;
     int depth;
   };
+
+  // One introsort step on [f, l): median-of-3 pivot to the front, unguarded
+  // partition; returns the cut (an index of a_).
+  size_t Cut(Elem* f, Elem* l) {
+    Elem* mid = f + (l - f) / 2;
+    MoveMedianToFirst(f, f + 1, mid, l - 1);
+    Elem* c = static_cast<size_t>(l - f) >= kParallelMin ? ParallelPartition(f, l)
+                                                          : UnguardedPartition(f + 1, l, f);
+    return static_cast<size_t>(c - a_);
+  }
+
+  // UnguardedPartition(f + 1, l, f) on the pool.  L[k]: the k-th position of
+  // [f + 1, l) (ascending) whose key is not below the pivot, R[k]: the k-th
+  // (descending) of [f, l) whose key is not above it.  While L[k] < R[k] the
+  // sequential loop swaps exactly these pairs (no scan meets a swapped
+  // position before the pointers cross); with K the first k where L[k] >=
+  // R[k], its last left scan stops at min(L[K], R[K - 1]) -- R[K - 1] now
+  // holds an element not below the pivot -- which is the cut.
+  Elem* ParallelPartition(Elem* f, Elem* l) {
+    const float pv = f->second;
+    const size_t n = static_cast<size_t>(l - f);
+    const int chunks = 64;
+    const size_t per = (n + chunks - 1) / chunks;
+    std::vector<size_t> nl(chunks + 1, 0), nr(chunks + 1, 0);
+    ParallelFor(chunks, [&](int c) {
+      size_t a = 0, b = 0;
+      for (size_t i = c * per; i < std::min(n, (c + 1) * per); ++i) {
+        const float k = f[i].second;
+        a += (i > 0 && !(k < pv)) ? 1 : 0;
+        b += !(pv < k) ? 1 : 0;
+      }
+      nl[c + 1] = a;
+      nr[c + 1] = b;
+    });
+    for (int c = 0; c < chunks; ++c) {
+      nl[c + 1] += nl[c];
+      nr[c + 1] += nr[c];
+    }
+    const size_t cl = nl[chunks], cr = nr[chunks];
+    std::vector<size_t> L(cl), R(cr);
+    ParallelFor(chunks, [&](int c) {
+      size_t a = nl[c], b = cr - nr[c];  // R descending: chunk c's last slot
+      for (size_t i = c * per; i < std::min(n, (c + 1) * per); ++i) {
+        const float k = f[i].second;
+        if (i > 0 && !(k < pv)) L[a++] = i;
+        if (!(pv < k)) R[--b] = i;
+      }
+    });
+    // K: first k with L[k] >= R[k] (L rises, R falls)
+    size_t lo = 0, hi = std::min(cl, cr);
+    while (lo < hi) {
+      const size_t m = lo + (hi - lo) / 2;
+      if (L[m] >= R[m]) hi = m; else lo = m + 1;
+    }
+    const size_t K = lo;
+    const int swap_chunks = static_cast<int>(std::min<size_t>(64, (K + 4095) / 4096));
+    if (swap_chunks > 0) {
+      const size_t sp = (K + swap_chunks - 1) / swap_chunks;
+      ParallelFor(swap_chunks, [&](int c) {
+        for (size_t k = c * sp; k < std::min(K, (c + 1) * sp); ++k) std::swap(f[L[k]], f[R[k]]);
+      });
+    }
+    size_t cut = K < cl ? L[K] : n;
+    if (K > 0) cut = std::min(cut, R[K - 1]);
+    return f + cut;
+  }
 
   static bool Less(const Elem& x, const Elem& y) { return x.second < y.second; }
 
