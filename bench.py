@@ -302,6 +302,54 @@ def cpu_baseline(width, height, quality, processes=8):
                 reference_bytes_match_manifest="%d/%d" % (matched, cores))
 
 
+def large_frame(gz, dist, world, rank, dev):
+    """BASELINE configs[4] after the timed region: one synthetic 8192x8192
+    frame at q=84 (seed 0, whose reference bytes are committed).  With N >= 4
+    GPUs it is split into 4 row strips with a halo over ranks 0-3 (their own
+    GPUs, RCCL all-gathers over xGMI: host/strips.h), else encoded by one
+    engine.  One untimed encode first (engine creation), then one timed;
+    wall time is the max over the participating ranks; bytes checked."""
+    import hashlib
+    import torch
+    w = h = 8192
+    q = 84
+    kn = known_answers(w, h, q).get(0)
+    rgb = gz.synthetic_frame(0, w, h)
+    params = gz.Params.for_quality(q)
+    strips = world >= 4
+    group = None
+    if strips:
+        group = dist.new_group([0, 1, 2, 3])
+        if rank >= 4:
+            return None
+        coll = gz.Collectives.from_torch(dist, "cuda:%d" % dev, group=group)
+
+        def run():
+            return gz.process_strips(rgb, w, h, coll, params, device=dev)
+    elif rank == 0:
+        def run():
+            return gz.process(rgb, w, h, params, device=dev)
+    else:
+        return None
+    run()  # (engine creation, first touch)
+    if strips:
+        dist.barrier(group=group)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    data = run()
+    elapsed = time.perf_counter() - t0
+    if strips:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        elapsed = float(t.item())
+    sha = hashlib.sha256(data).hexdigest()
+    return {"config": "BASELINE configs[4]: synthetic 8192x8192 q84 (seed 0)",
+            "mode": "4 row strips + halo over GPUs 0-3 (RCCL)" if strips else "one engine, 1 GPU",
+            "gpus": 4 if strips else 1, "seconds": round(elapsed, 3),
+            "Mpixels_per_s": round(w * h / elapsed / 1e6, 3), "bytes": len(data),
+            "bit_exact": bool(kn and kn[0] == sha), "against": "reference guetzli --c sha256"}
+
+
 def dist_selftest(args):
     """The multi-rank skeleton of main() on CPU: every rank (launched by
     launch_ranks) joins a gloo group, "encodes" its frames into stand-in byte
@@ -345,6 +393,9 @@ def main():
                     help="frames encoded at once per GPU (0: all frames of the step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-processes", type=int, default=8)
+    ap.add_argument("--no-large-frame", action="store_true",
+                    help="skip the BASELINE configs[4] leg (8192x8192 q84: one engine at N < 4, "
+                         "4 row strips over GPUs 0-3 at N >= 4)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU check of the multi-rank path (launcher, gloo, byte gather, "
                          "max-over-ranks timing) with stand-in payloads; no GPU")
@@ -458,6 +509,7 @@ def main():
         host[k] = getattr(st1, k)
     host.update(gz.last_process_detail())
 
+    large = None if args.no_large_frame else large_frame(gz, dist, world, rank, dev)
     if rank != 0:
         pool.shutdown()
         if dist is not None:
@@ -573,6 +625,8 @@ def main():
                          "iterations": st1.iterations,
                          "host_breakdown_seconds": {k: round(v, 4) for k, v in host.items()}},
     }
+    if large is not None:
+        out["configs4_8192"] = large
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(w, h, q, args.cpu_baseline_processes)
     print(json.dumps(out), flush=True)

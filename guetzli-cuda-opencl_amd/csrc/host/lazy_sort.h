@@ -105,7 +105,10 @@ class LazyStdSort {
 
  private:
   static constexpr size_t kThreshold = 16;
-  static constexpr size_t kParallelMin = size_t{1} << 16;  // ranges partitioned on the pool
+  // ranges partitioned on the pool: only large frames' (the parallel form
+  // does ~3x the sequential work; below this the pool's latency gain is not
+  // worth its CPU when several encodes share the pool)
+  static constexpr size_t kParallelMin = size_t{1} << 20;
   struct Range {
     size_t lo, hi;
     int depth;

@@ -1276,10 +1276,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       if (bulk) {
         const auto tbk = Clock::now();
         sorter.SetPrefix(bulk);
+        res_->detail["backend_setprefix_s"] += Since(tbk);
+        // per-block counts of the prefix's owned entries (parallel; blocks
+        // are spread, so the atomic increments rarely meet)
         bulk_cnt_.assign(num_blocks, 0);
-        for (size_t i = 0; i < bulk; ++i) {
-          const int b = global_order[i].first - gbase;
-          if (b >= own_lo && b < own_hi) ++bulk_cnt_[b];
+        {
+          const int kSlices = bulk >= (size_t{1} << 18) ? 64 : 1;
+          int* cnt = bulk_cnt_.data();
+          ParallelFor(kSlices, [&](int sl) {
+            for (size_t i = bulk * sl / kSlices; i < bulk * (sl + 1) / kSlices; ++i) {
+              const int b = global_order[i].first - gbase;
+              if (b >= own_lo && b < own_hi) __atomic_fetch_add(&cnt[b], 1, __ATOMIC_RELAXED);
+            }
+          });
         }
         struct ChunkDelta {
           JpegHistogram h[3];
@@ -1522,47 +1531,78 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
 // owned ones (each rank sends its keys and an entry count per owned block;
 // the pairs are rebuilt in rank order, which is block order).  *entries holds
 // this rank's on entry, the frame's on return; *blocks_to_change becomes the
-// frame's count.
+// frame's count.  Packing and unpacking run on the host pool.
 bool Processor::GatherEntries(std::vector<std::pair<int, float>>* entries, int own_lo, int own_hi,
                               int gbase, int* blocks_to_change) {
   const int nown = own_hi - own_lo;
-  std::vector<uint8_t> send(8 + nown + entries->size() * 4, 0);
-  const uint32_t n = static_cast<uint32_t>(entries->size()), btc = static_cast<uint32_t>(*blocks_to_change);
-  std::memcpy(send.data(), &n, 4);
+  const size_t n = entries->size();
+  std::vector<uint8_t> send(8 + nown + n * 4, 0);
+  const uint32_t n32 = static_cast<uint32_t>(n), btc = static_cast<uint32_t>(*blocks_to_change);
+  std::memcpy(send.data(), &n32, 4);
   std::memcpy(send.data() + 4, &btc, 4);
   uint8_t* cnt = send.data() + 8;
-  float* keys = reinterpret_cast<float*>(send.data() + 8 + nown);
-  for (size_t i = 0; i < entries->size(); ++i) {
-    ++cnt[(*entries)[i].first - gbase - own_lo];
-    std::memcpy(keys + i, &(*entries)[i].second, 4);
-  }
+  uint8_t* keys = send.data() + 8 + nown;
+  constexpr int kSlices = 64;
+  ParallelFor(kSlices, [&](int sl) {
+    // (entries of one block are contiguous; a slice counts the blocks whose
+    // first entry it holds, through the block's end)
+    size_t i = n * sl / kSlices;
+    const size_t end = n * (sl + 1) / kSlices;
+    if (i > 0)
+      while (i < end && (*entries)[i].first == (*entries)[i - 1].first) ++i;
+    while (i < end) {
+      const int b = (*entries)[i].first;
+      size_t k = i;
+      while (k < n && (*entries)[k].first == b) {
+        std::memcpy(keys + 4 * k, &(*entries)[k].second, 4);
+        ++k;
+      }
+      cnt[b - gbase - own_lo] = static_cast<uint8_t>(k - i);
+      i = k;
+    }
+  });
   std::vector<std::vector<uint8_t>> all;
   if (!part_->coll->AllGatherV(send, &all)) return false;
-  size_t total = 0;
+  const int world = part_->world, bw = part_->bw;
+  std::vector<size_t> rank_at(world + 1, 0);
   int frame_btc = 0;
-  for (const auto& m : all) {
+  for (int r = 0; r < world; ++r) {
     uint32_t v;
-    std::memcpy(&v, m.data(), 4);
-    total += v;
-    std::memcpy(&v, m.data() + 4, 4);
+    std::memcpy(&v, all[r].data(), 4);
+    rank_at[r + 1] = rank_at[r] + v;
+    std::memcpy(&v, all[r].data() + 4, 4);
     frame_btc += static_cast<int>(v);
   }
-  entries->resize(total);
-  size_t at = 0;
-  for (int r = 0; r < part_->world; ++r) {
-    const std::vector<uint8_t>& m = all[r];
-    const int b0 = part_->row0[r] * part_->bw, nb = (part_->row0[r + 1] - part_->row0[r]) * part_->bw;
-    const uint8_t* c = m.data() + 8;
-    const uint8_t* k = m.data() + 8 + nb;
-    for (int b = 0; b < nb; ++b)
+  entries->resize(rank_at[world]);
+  // work items: (rank, 4096-block chunk), each filling its own range
+  constexpr int kChunk = 4096;
+  std::vector<std::pair<int, int>> items;
+  std::vector<size_t> item_at;
+  for (int r = 0; r < world; ++r) {
+    const int nb = (part_->row0[r + 1] - part_->row0[r]) * bw;
+    const uint8_t* c = all[r].data() + 8;
+    size_t at = rank_at[r];
+    for (int b0 = 0; b0 < nb; b0 += kChunk) {
+      items.emplace_back(r, b0);
+      item_at.push_back(at);
+      for (int b = b0; b < std::min(nb, b0 + kChunk); ++b) at += c[b];
+    }
+  }
+  ParallelFor(static_cast<int>(items.size()), [&](int it) {
+    const int r = items[it].first, b0 = items[it].second;
+    const int nb = (part_->row0[r + 1] - part_->row0[r]) * bw, base = part_->row0[r] * bw;
+    const uint8_t* c = all[r].data() + 8;
+    size_t at = item_at[it];
+    const uint8_t* k = all[r].data() + 8 + nb + 4 * (at - rank_at[r]);
+    for (int b = b0; b < std::min(nb, b0 + kChunk); ++b)
       for (int j = 0; j < c[b]; ++j, ++at, k += 4) {
         float key;
         std::memcpy(&key, k, 4);
-        (*entries)[at] = std::make_pair(b0 + b, key);
+        (*entries)[at] = std::make_pair(base + b, key);
       }
-  }
+  });
   *blocks_to_change = frame_btc;
-  return at == total;
+  return true;
 }
 
 // RemoveOriginalQuantization, processor.cc:94-107: coefficients times their

@@ -441,7 +441,7 @@ class Collectives:
         self._c = _Collectives(None, rank, world, self._cb)
 
     @classmethod
-    def from_torch(cls, dist, device="cpu"):
+    def from_torch(cls, dist, device="cpu", group=None):
         """Bound to torch.distributed: all_gather_into_tensor of uint8 blocks on
         `device` ("cuda:N" for RCCL over xGMI with the nccl backend, "cpu" for
         gloo).  The library's buffers are wrapped, not copied: on the CPU the
@@ -449,7 +449,7 @@ class Collectives:
         the block and one D2H copy of the result."""
         import torch
 
-        world, rank = dist.get_world_size(), dist.get_rank()
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
 
         def wrap(ptr, n):
             return torch.frombuffer((ctypes.c_uint8 * n).from_address(ptr), dtype=torch.uint8)
@@ -459,11 +459,11 @@ class Collectives:
                 return
             src, dst = wrap(send, n), wrap(recv, n * world)
             if str(device) == "cpu":
-                dist.all_gather(list(dst.view(world, n).unbind(0)), src)
+                dist.all_gather(list(dst.view(world, n).unbind(0)), src, group=group)
             else:
                 d_src = src.to(device, non_blocking=False)
                 d_dst = torch.empty(world * n, dtype=torch.uint8, device=device)
-                dist.all_gather_into_tensor(d_dst, d_src)
+                dist.all_gather_into_tensor(d_dst, d_src, group=group)
                 dst.copy_(d_dst)
 
         return cls(rank, world, allgather_into=allgather_into)

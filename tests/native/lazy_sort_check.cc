@@ -13,7 +13,7 @@ int main(int argc, char** argv) {
   const unsigned seed = argc > 1 ? atoi(argv[1]) : 1;
   std::mt19937 rng(seed);
   int bad = 0, cases = 0;
-  for (int n : {0, 1, 2, 3, 15, 16, 17, 33, 100, 1000, 4097, 100000, 300000, 2000000}) {
+  for (int n : {0, 1, 2, 3, 15, 16, 17, 33, 100, 1000, 4097, 100000, 300000, 3000000}) {
     for (int distinct : {1, 2, 7, 100, 1 << 30}) {
       std::vector<std::pair<int, float>> a(n);
       for (int i = 0; i < n; ++i)
