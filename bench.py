@@ -101,10 +101,24 @@ PASS_KERNELS = ("coeffs_to_linear", "opsin_mhic", "edge_mask", "block_diff", "bl
                 "combine_channels", "diffmap_blur_h", "diffmap_blur_v", "diffmap_final")
 
 
+# The device entropy coder, per MCU (4:4:4: one 8x8 block per component):
+# k_jpeg_stage reads the 3 x 64 int16 coefficients and writes their 3 x 64
+# int16 quantized zigzag copies and 3 non-zero masks (u64); k_jpeg_code reads
+# the zigzag coefficients (the scan it writes, ~2-5 % of that at q95, is not
+# counted; its per-workgroup code table copies are L2 traffic).
+JPEG_STAGE_BYTES_PER_MCU = 3 * 64 * 2 * 2 + 3 * 8
+JPEG_CODE_BYTES_PER_MCU = 3 * 64 * 2
+
+
 def region_bytes(name, w, h):
     """Algorithmic HBM bytes per launch of a profiled region, or None."""
+    blocks = ((w + 7) // 8) * ((h + 7) // 8)
     if name == "block_zeroing":
-        return ZEROING_BYTES_PER_BLOCK * ((w + 7) // 8) * ((h + 7) // 8)
+        return ZEROING_BYTES_PER_BLOCK * blocks
+    if name == "jpeg_stage":
+        return JPEG_STAGE_BYTES_PER_MCU * blocks
+    if name == "jpeg_code":
+        return JPEG_CODE_BYTES_PER_MCU * blocks
     bpp = stage_bytes_per_px()
     return bpp[name] * w * h if name in bpp else None
 
@@ -131,7 +145,8 @@ STAGE_SYMBOL = {
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
     "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
     "combine_channels": "gz::k_combine_channels(",
-    "block_zeroing": "gz::k_block_zeroing(",
+    "block_zeroing": "gz::k_block_zeroing(", "jpeg_stage": "gz::k_jpeg_stage(",
+    "jpeg_code": "gz::k_jpeg_code(",
     "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
 }
 
@@ -529,7 +544,7 @@ def main():
         row = {"launches": cnt, "avg_ms": round(avg, 4), "frame_ms": round(ms, 4)}
         if b is not None:
             row["algo_GBps"] = round(b / (avg * 1e-3) / 1e9, 1)
-        if name in bpp or name == "block_zeroing":
+        if name in bpp or name in ("block_zeroing", "jpeg_stage", "jpeg_code"):
             stages[name] = row
         if name != "compare_pass":
             regions.append((ms, name, cnt))

@@ -1102,7 +1102,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
-                                     nullptr, tr));
+                                     nullptr, tr, 0));
   BzTraceDump(tr, nb_, stream_);
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
@@ -1122,19 +1122,25 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
   GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                      comp_mask, limit, lookahead, new_model ? 1 : 0,
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
-                                     nullptr, tr));
+                                     nullptr, tr, 1));
   BzTraceDump(tr, nb_, stream_);
-  return CompactCandidates(nb_, limit, offsets, idx, err);
+  return CompactCandidates(nb_, limit, offsets, idx, err, true);
 }
 
 // The kept entries of the first nblocks blocks' orders (d_zero_out_ /
 // d_zero_count_), concatenated, to the host.
 bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
-                               std::vector<uint8_t>* idx, std::vector<float>* err) {
+                               std::vector<uint8_t>* idx, std::vector<float>* err, bool slots) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (!ScanCounts(d_zero_count_, nblocks, d_zero_off_, "scan_counts")) return false;
-  GZ_TIMED("compact_candidates", k_compact_candidates<<<(nblocks + 3) / 4, 256, 0, s>>>(
-      static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nblocks, limit, d_cand_idx_, d_cand_err_));
+  if (slots) {
+    GZ_TIMED("compact_candidates", k_compact_slots<<<(nblocks + 3) / 4, 256, 0, s>>>(
+        static_cast<const uint8_t*>(d_zero_out_), d_zero_count_, d_zero_off_, nblocks, d_cand_idx_,
+        d_cand_err_));
+  } else {
+    GZ_TIMED("compact_candidates", k_compact_candidates<<<(nblocks + 3) / 4, 256, 0, s>>>(
+        static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nblocks, limit, d_cand_idx_, d_cand_err_));
+  }
   GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nblocks + 1) * 4, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   const size_t total = static_cast<size_t>(h_zero_off_[nblocks]);
@@ -1204,8 +1210,8 @@ bool Engine::BlockZeroingCandidates420(int comp_mask, float limit, int lookahead
     if (!OrderBlocks(1)) return false;
     GZ_TIMED("block_zeroing", k_block_zeroing<<<nb_, 64, BzLdsPad(), s>>>(
         d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_, 1, limit, lookahead, new_model ? 1 : 0,
-        static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_, d_planes_, nullptr));
-    return CompactCandidates(nb_, limit, offsets, idx, err);
+        static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_, d_planes_, nullptr, 1));
+    return CompactCandidates(nb_, limit, offsets, idx, err, true);
   }
   if (comp_mask != 6) return Fail("BlockZeroingCandidates420 comp_mask", 0);
   // wavefronts t = bx + 2 by (block_zeroing420.inc); by in

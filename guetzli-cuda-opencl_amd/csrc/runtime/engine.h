@@ -208,8 +208,9 @@ class Engine {
   // d_mb_ first; false when the Compare pass's fused edge_mask made it).
   bool MaskPipeline(const float* xyb0, const float* xyb1, bool sub_b, bool front = true);
   bool EnqueueCompare(CompareDebug* dbg);
+  // slots: k_block_zeroing's kept entries per block (else CoeffData orders)
   bool CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
-                         std::vector<uint8_t>* idx, std::vector<float>* err);
+                         std::vector<uint8_t>* idx, std::vector<float>* err, bool slots = false);
   // what Compare's first stage reads (and its hipGraphExec_t each)
   enum CandSource { kCandCoeffs = 0, kCand420 = 1, kCandRgb = 2 };
   int cand_src_ = kCandCoeffs;
