@@ -171,33 +171,91 @@ def measured_traffic(stage, w, h):
     return None, None
 
 
-# gfx950 vector issue: a wave64 VALU instruction occupies its SIMD-32 for 2
-# cycles (MI355X_MICROARCH.md, execution model); 256 CUs x 4 SIMDs, 2.4 GHz.
+# gfx950 vector issue: a wave64 VALU instruction occupies its SIMD for 2
+# cycles at full rate (MI355X_MICROARCH.md, execution model); 256 CUs x 4
+# SIMDs, 2.4 GHz.  FP64 and transcendental instructions issue slower: their
+# cycles per wave instruction come from the micro-benchmark
+# tools/micro/valu_rate.hip (profiles/round3_valu_rate.json: fma_f64 4.95,
+# mul_f64 4.59, add_f64 4.36, rsq_f64 16.1, ...), and the PMC summaries carry
+# gfx950's per-type instruction counters (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_
+# {F32,F64}, _INT32, _INT64, _CVT), so the ceiling weights each type by its
+# measured cost; untyped instructions (moves, logic, compares, selects) count
+# at the full-rate 2 cycles.
 VALU_SIMDS, VALU_CYCLES_PER_INST, CLOCK_HZ = 1024, 2, 2.4e9
+# counter -> micro-benchmark entry (cycles per wave instruction)
+VALU_TYPE_RATE = {
+    "SQ_INSTS_VALU_ADD_F64": "add_f64", "SQ_INSTS_VALU_MUL_F64": "mul_f64",
+    "SQ_INSTS_VALU_FMA_F64": "fma_f64", "SQ_INSTS_VALU_TRANS_F64": "rsq_f64",
+    "SQ_INSTS_VALU_TRANS_F32": "rsq_f32", "SQ_INSTS_VALU_FMA_F32": "fma_f32",
+    "SQ_INSTS_VALU_ADD_F32": "add_f32", "SQ_INSTS_VALU_MUL_F32": "fma_f32",
+    "SQ_INSTS_VALU_INT32": "mul_u32", "SQ_INSTS_VALU_CVT": "cvt_f64_f32_pair",
+}
+
+
+def valu_rates():
+    """{micro-benchmark entry: cycles per wave instruction} from the newest
+    committed profiles/*valu_rate*.json ({} when none)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*valu_rate*.json")), reverse=True):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        out = {k: v["cycles_per_wave_inst"] for k, v in t.items() if isinstance(v, dict)}
+        if "cvt_f64_f32_pair" in out:  # two conversions per timed step
+            out["cvt_f64_f32_pair"] /= 2
+        out["_source"] = os.path.relpath(f, ROOT)
+        return out
+    return {}
 
 
 def valu_issue(stage, w, h, avg_ms):
-    """VALU issue utilisation of `stage`'s kernel: its measured vector
-    instructions per launch (SQ_INSTS_VALU, committed rocprofv3 PMC summary
-    profiles/*pmc_util_<WxH>.json) x 2 cycles over all SIMDs, against the
-    launch's HIP-event duration -- how close a VALU-bound kernel is to the
-    vector issue ceiling (the HBM roofline does not bound it)."""
+    """VALU issue utilisation of `stage`'s kernel against the launch's
+    HIP-event duration: its measured vector instructions per launch
+    (committed rocprofv3 PMC summary profiles/*pmc_util_<WxH>.json) x their
+    issue cycles over all SIMDs -- how close a VALU-bound kernel is to the
+    vector issue ceiling (the HBM roofline does not bound it).  `frac` uses
+    the per-type cycle costs where the summary has the typed counters
+    (FP64 at ~4.4-5 cycles, see VALU_TYPE_RATE); `frac_flat` counts every
+    instruction at 2 cycles."""
     import glob
     sym = STAGE_SYMBOL.get(stage)
     if sym is None:
         return None
     sym = sym.split("(")[0]
+    rates = valu_rates()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_util*%dx%d*.json" % (w, h))),
                     reverse=True):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        v = t.get(sym, {}).get("SQ_INSTS_VALU")
-        if v:
-            busy = v * VALU_CYCLES_PER_INST / VALU_SIMDS / CLOCK_HZ
-            return {"valu_insts_per_launch": int(v), "issue_ms": round(busy * 1e3, 4),
-                    "frac": round(busy / (avg_ms * 1e-3), 4), "source": os.path.relpath(f, ROOT)}
+        k = t.get(sym, {})
+        v = k.get("SQ_INSTS_VALU")
+        if not v:
+            continue
+        flat = v * VALU_CYCLES_PER_INST / VALU_SIMDS / CLOCK_HZ
+        r = {"valu_insts_per_launch": int(v), "issue_ms_flat": round(flat * 1e3, 4),
+             "frac_flat": round(flat / (avg_ms * 1e-3), 4), "source": os.path.relpath(f, ROOT)}
+        typed = {c: k[c] for c in VALU_TYPE_RATE if c in k}
+        if typed and all(VALU_TYPE_RATE[c] in rates for c in typed):
+            cyc, rest = 0.0, float(v)
+            for c, n in typed.items():
+                cyc += n * rates[VALU_TYPE_RATE[c]]
+                rest -= n
+            cyc += max(rest, 0.0) * VALU_CYCLES_PER_INST
+            busy = cyc / VALU_SIMDS / CLOCK_HZ
+            f64 = sum(k.get(c, 0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                           "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+            r.update({"issue_ms": round(busy * 1e3, 4), "frac": round(busy / (avg_ms * 1e-3), 4),
+                      "fp64_inst_share": round(f64 / v, 4),
+                      "fp64_cycle_share": round(sum(k.get(c, 0) * rates[VALU_TYPE_RATE[c]] for c in (
+                          "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                          "SQ_INSTS_VALU_TRANS_F64")) / cyc, 4),
+                      "rates_source": rates["_source"]})
+        else:
+            r.update({"issue_ms": r["issue_ms_flat"], "frac": r["frac_flat"]})
+        return r
     return None
 
 

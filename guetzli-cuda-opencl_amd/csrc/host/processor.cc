@@ -357,10 +357,18 @@ bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const
   Engine* e = engine_.get();
   uint32_t hist[6 * 256];
   uint64_t chroma = 0;
-  if (!e->JpegStageEnqueue(img.quant) || !e->CompareEnqueue() || !e->JpegStageWait(hist, &chroma)) {
+  if (!e->JpegStageEnqueue(img.quant) || !e->CompareEnqueue()) {
     err_ = e->error();
     return false;
   }
+  const auto tw0 = Clock::now();
+  const double cw0 = ThreadCpu();
+  if (!e->JpegStageWait(hist, &chroma)) {
+    err_ = e->error();
+    return false;
+  }
+  seconds_wait += Since(tw0);
+  cpu_wait += ThreadCpu() - cw0;
   JpegHistogram dc_h[3], ac_h[3];
   const int ncomp = HistogramsFromStage(hist, chroma, dc_h, ac_h);
   JpegCodeTables codes;
@@ -385,10 +393,18 @@ bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const
   }
   seconds_encode += Since(t0);
   uint64_t nbits = 0, ff = 0;
-  if (!e->JpegScanEnqueue(ncomp, codes) || !e->Sync() || !e->JpegScanFinish(&nbits, &ff)) {
+  if (!e->JpegScanEnqueue(ncomp, codes)) {
     err_ = e->error();
     return false;
   }
+  const auto tw1 = Clock::now();
+  const double cw1 = ThreadCpu();
+  if (!e->Sync() || !e->JpegScanFinish(&nbits, &ff)) {
+    err_ = e->error();
+    return false;
+  }
+  seconds_wait += Since(tw1);
+  cpu_wait += ThreadCpu() - cw1;
   e->CompareFinish(&distance_, block_max_.data());
   ++compares;
   // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
@@ -1095,8 +1111,11 @@ bool Processor::SelectFrequencyMasking(const JpegData& jpg, CoeffImage* img, int
     return Fail(err);
   cmp_->FinishBlockComparisons();
   res_->detail["candidates"] = static_cast<double>(cand.size());
-  return SelectFrequencyBackEnd(jpg, img, comp_mask, target_mul, stop_early, offsets, cand,
-                                cand_err, err);
+  const double c0 = ThreadCpu();
+  const bool ok = SelectFrequencyBackEnd(jpg, img, comp_mask, target_mul, stop_early, offsets, cand,
+                                         cand_err, err);
+  res_->detail["backend_thread_cpu_s"] += ThreadCpu() - c0;
+  return ok;
 }
 
 bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int comp_mask,
@@ -1298,9 +1317,42 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         ParallelFor(own_chunks, [&](int ch) {
           ChunkDelta& d = deltas[ch];
           int64_t raw_unused = 0;
-          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
+          const int b0 = own_lo + ch * kOrderChunk, b1 = std::min(own_hi, b0 + kOrderChunk);
+          size_t total = 0;
+          for (int bix = b0; bix < b1; ++bix) total += bulk_cnt_[bix];
+          d.changed.reserve(total);
+          // the touched blocks are scattered over three 2-byte-per-coefficient
+          // planes much larger than the caches: fetch a block a few touched
+          // blocks ahead (its first change's plane, the mask word, and for
+          // direction < 0 the original coefficients)
+          constexpr int kAhead = 6;
+          auto prefetch = [&](int b) {
+            const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
+            const int ci = off + last_indexes[b] + std::min(direction, 0);
+            if (ci < 0 || ci >= static_cast<int>(cand.size())) return;
+            const int c = cand[ci] / kDCTBlockSize;
+            const coeff_t* blk = img->block(c, b);
+            __builtin_prefetch(blk, 1);
+            __builtin_prefetch(blk + 32, 1);
+            __builtin_prefetch(&acm.nz[static_cast<size_t>(c) * num_blocks + b], 1);
+            if (direction < 0) {
+              const JpegComponent& comp = jpg.components[c];
+              const coeff_t* o = comp.coeffs.data() +
+                                 static_cast<size_t>((b / block_width) * comp.width_in_blocks + b % block_width) * 64;
+              __builtin_prefetch(o);
+              __builtin_prefetch(o + 32);
+            }
+          };
+          int ahead = b0, pending = 0;  // next block to prefetch; touched blocks in flight
+          for (int bix = b0; bix < b1; ++bix) {
+            for (; ahead < b1 && pending < kAhead; ++ahead)
+              if (bulk_cnt_[ahead]) {
+                prefetch(ahead);
+                ++pending;
+              }
             const int cnt = bulk_cnt_[bix];
             if (!cnt) continue;
+            --pending;
             const int bx = bix % block_width, by = bix / block_width;
             const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
             for (int t = 0; t < cnt; ++t) {
@@ -2094,6 +2146,8 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
     result->seconds_compare = cmp->seconds_compare;
     result->seconds_zeroing = cmp->seconds_zeroing;
     result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
+    result->detail["compare_wait_s"] = cmp->seconds_wait;
+    result->detail["compare_wait_cpu_s"] = cmp->cpu_wait;
   }
   result->seconds_total = Since(t0);
   result->detail["thread_cpu_s"] = ThreadCpu() - c0;
@@ -2152,6 +2206,8 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     result->seconds_compare = cmp->seconds_compare;
     result->seconds_zeroing = cmp->seconds_zeroing;
     result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
+    result->detail["compare_wait_s"] = cmp->seconds_wait;
+    result->detail["compare_wait_cpu_s"] = cmp->cpu_wait;
   }
   result->seconds_total = Since(t0);
   result->detail["thread_cpu_s"] = ThreadCpu() - c0;

@@ -211,6 +211,7 @@ class HipButteraugliComparator : public Comparator {
   bool Sync(const CoeffImage& img) { return SyncCoeffs(img); }
   double seconds_compare = 0.0;
   double cpu_compare = 0.0;  // calling thread's CPU seconds in the compares
+  double seconds_wait = 0.0, cpu_wait = 0.0;  // of which waiting for the device (wall, CPU)
   double seconds_zeroing = 0.0;
   int compares = 0;
 

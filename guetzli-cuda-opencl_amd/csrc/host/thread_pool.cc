@@ -32,6 +32,11 @@ struct Job {
   int n;
   std::atomic<int> next{0};
   std::atomic<int> done{0};
+  // the owner's wait: per job, so a finishing job wakes its owner only (not
+  // every other frame's caller)
+  std::mutex done_mu;
+  std::condition_variable done_cv;
+  bool finished = false;  // set under done_mu by the last item's thread
 };
 
 class Pool {
@@ -50,21 +55,26 @@ class Pool {
       std::lock_guard<std::mutex> lk(mu_);
       it = jobs_.insert(jobs_.end(), &job);
     }
-    cv_.notify_all();
+    // wake as many workers as there are items for them (the caller takes
+    // one): a notify_all per call would wake every idle worker of the
+    // process for each of the hundreds of small passes a frame makes, most
+    // of them only to find nothing left and sleep again
+    const int wake = std::min(n - 1, static_cast<int>(threads_.size()));
+    for (int i = 0; i < wake; ++i) cv_.notify_one();
     Work(&job);
     {
       std::lock_guard<std::mutex> lk(mu_);
       jobs_.erase(it);  // no worker can pick it up any more
     }
     // items claimed by workers may still be running
-    std::unique_lock<std::mutex> lk(done_mu_);
-    done_cv_.wait(lk, [&] { return job.done.load() == n; });
+    std::unique_lock<std::mutex> lk(job.done_mu);
+    job.done_cv.wait(lk, [&] { return job.finished; });
   }
 
  private:
   // Runs claimed item i of `job` and then further items until none is left.
   // The next item is claimed BEFORE the current one is counted as done: the
-  // owner (who waits for done == n) keeps the job alive while this thread
+  // owner (who waits for the last count) keeps the job alive while this thread
   // holds an uncounted item, and the job is not touched after the last count.
   void Drain(Job* job, int i) {
     const int n = job->n;
@@ -73,8 +83,12 @@ class Pool {
       (*fn)(i);
       const int next = job->next.fetch_add(1);
       if (job->done.fetch_add(1) + 1 == n) {
-        std::lock_guard<std::mutex> lk(done_mu_);
-        done_cv_.notify_all();
+        // (the owner returns -- and destroys the job -- only after seeing
+        // `finished` under the job's mutex, i.e. after this thread's last
+        // touch of the job, the unlock)
+        std::lock_guard<std::mutex> lk(job->done_mu);
+        job->finished = true;
+        job->done_cv.notify_one();
       }
       i = next;
     }
@@ -108,8 +122,6 @@ class Pool {
   std::mutex mu_;
   std::condition_variable cv_;
   std::list<Job*> jobs_;
-  std::mutex done_mu_;
-  std::condition_variable done_cv_;
 };
 
 Pool* GetPool() {

@@ -53,13 +53,17 @@ def _native_bin(name, with_oracle):
         os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith(".h")]
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = "%s.%d.tmp" % (out, os.getpid())
         cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread",
                "-I", os.path.join(ROOT, "guetzli-cuda-opencl_amd", "csrc"),
                "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
-               src, "-o", out, "-L", lib_dir, "-lguetzli_hip", "-Wl,-rpath," + lib_dir]
+               src, "-o", tmp, "-L", lib_dir, "-lguetzli_hip", "-Wl,-rpath," + lib_dir]
         if with_oracle:
             cmd += ["-L", oracle_dir, "-lgz_oracle", "-Wl,-rpath," + oracle_dir]
         subprocess.run(cmd, check=True)
+        # (pytest-xdist workers may build the same binary at once: each links
+        # its own file and renames it into place, so none runs a partial one)
+        os.replace(tmp, out)
     return out
 
 

@@ -1,7 +1,8 @@
 // VALU issue cost per wave64 instruction on gfx950, by type: the ceiling
 // bench.py's valu_issue weights k_block_zeroing's instruction mix with
 // (FP64 adds / multiplies / FMAs / square roots next to FP32 and integer
-// ops).  Each kernel runs 8 independent dependency chains per lane (enough
+// ops; cvt_f64_f32_pair is a v_cvt_f32_f64 + v_cvt_f64_f32 pair, two
+// instructions per step).  Each kernel runs 8 independent dependency chains per lane (enough
 // to hide the pipeline latency) over enough waves to fill every SIMD several
 // times; cycles per instruction per SIMD = SIMDs x clock x seconds /
 // (wave instructions).  Prints one JSON object.
@@ -37,6 +38,9 @@ __global__ __launch_bounds__(256) void k_rate(double* out, float* outf, int* out
       else if constexpr (kOp == 4) f[c] = fmaf(f[c], mf, 1e-7f);  // v_fma_f32
       else if constexpr (kOp == 5) n[c] = n[c] * 747796405 + 1;   // v_mad_u32_u24 / v_mul_lo
       else if constexpr (kOp == 6) a[c] = __builtin_amdgcn_rsq(a[c]);  // v_rsq_f64 (transcendental)
+      else if constexpr (kOp == 7) f[c] = __builtin_amdgcn_rsqf(f[c]);  // v_rsq_f32 (transcendental)
+      else if constexpr (kOp == 8) f[c] = f[c] + mf;                    // v_add_f32
+      else if constexpr (kOp == 9) a[c] = static_cast<double>(static_cast<float>(a[c]));  // cvt f64<->f32
     }
   }
   double r = 0.0;
@@ -69,9 +73,10 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  const char* names[] = {"fma_f64", "mul_f64", "add_f64", "sqrt_f64", "fma_f32", "mul_u32", "rsq_f64"};
+  const char* names[] = {"fma_f64", "mul_f64", "add_f64", "sqrt_f64", "fma_f32", "mul_u32", "rsq_f64",
+                         "rsq_f32", "add_f32", "cvt_f64_f32_pair"};
   printf("{\"cus\": %d, \"clock_mhz\": %.0f", cus, clock_hz / 1e6);
-  for (int op = 0; op < 7; ++op) {
+  for (int op = 0; op < 10; ++op) {
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
       (void)hipEventRecord(e0);
@@ -82,7 +87,10 @@ int main() {
         case 3: k_rate<3><<<blocks, 256>>>(d, df, di, 1e-9); break;
         case 4: k_rate<4><<<blocks, 256>>>(d, df, di, 1e-9); break;
         case 5: k_rate<5><<<blocks, 256>>>(d, df, di, 1e-9); break;
-        default: k_rate<6><<<blocks, 256>>>(d, df, di, 1e-9); break;
+        case 6: k_rate<6><<<blocks, 256>>>(d, df, di, 1e-9); break;
+        case 7: k_rate<7><<<blocks, 256>>>(d, df, di, 1e-9); break;
+        case 8: k_rate<8><<<blocks, 256>>>(d, df, di, 1e-9); break;
+        default: k_rate<9><<<blocks, 256>>>(d, df, di, 1e-9); break;
       }
       (void)hipEventRecord(e1);
       (void)hipEventSynchronize(e1);
