@@ -224,11 +224,14 @@ def test_compare_matches_oracle_on_synthetic(gz, w, h, seed):
     assert np.float32(st["distance"]) == np.float32(d)
 
 
-@pytest.mark.parametrize("w,h,seed", [(256, 256, 7), (333, 197, 8), (517, 389, 4)])
+@pytest.mark.parametrize("w,h,seed", [(256, 256, 7), (333, 197, 8), (517, 389, 4), (700, 301, 5),
+                                      (519, 250, 6), (518, 45, 2)])
 def test_compare_fast_path_matches_oracle(gz, w, h, seed):
     """The Compare pass as the search runs it (graph-launched, no stage dumps,
     the B activity mask evaluated only where CombineChannels samples it):
-    distance and per-block maxima equal the CPU oracle's."""
+    distance and per-block maxima equal the CPU oracle's.  Sizes cover both
+    parities of the (w-5)x(h-5) crop, a last 128-column blur group of one
+    column (519) and rows / columns past the blurred grid."""
     L = oracle()
     rgb = gz.synthetic_frame(seed, w, h)
     coeffs = gz.rgb_to_coeffs(rgb, w, h)
