@@ -789,6 +789,52 @@ size_t ComputeEntropyCodes(const std::vector<JpegHistogram>& histograms, std::ve
 // removed and re-added (same counts as the full rescans).  raw_bits tracks
 // sum_i (counts[i]/2) * (depth[i] + (i & 0xf)) -- HistogramEntropyCost
 // before rounding -- for the current depths.
+// The change loop's control for one back-end iteration (processor.cc:
+// 836-905), shared by the 4:4:4 and the 4:2:0 back ends: the thresholds
+// from the iteration's order, the decades whose entropy codes are read, when
+// the size estimate is read and the break test.  The estimate is only read
+// once changed > min_coeffs (and at the last step), and a decade's codes
+// only if such a step reads them, so the codes of other decades are never
+// built -- the same values wherever they are read.
+struct ChangeLoop {
+  size_t n_order;
+  int min_coeffs;  // min_coeffs_to_change
+  double min_size_delta;
+  int changed = 0;
+  float val_threshold = 0.0f;
+  // factor: the searched blocks' size in 8x8 blocks (4:2:0 chroma: 2);
+  // *first_up_iter: the first up iteration's floor on min_coeffs (the count
+  // of keys below 0.75 x the block error limit), then cleared.
+  ChangeLoop(int direction, bool distance_ok, int base_size, int factor, int blocks_to_change,
+             bool* first_up_iter, float block_error_limit,
+             const std::vector<std::pair<int, float>>& order)
+      : n_order(order.size()) {
+    double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
+    if (direction > 0 && distance_ok) rel_size_delta = 0.05;
+    min_size_delta = base_size * rel_size_delta;
+    const float per_block = direction > 0 ? 2.0f : factor * factor * 0.2f;
+    min_coeffs = static_cast<int>(per_block * blocks_to_change);
+    if (*first_up_iter) {
+      const float limit = 0.75f * block_error_limit;
+      // partition_point(key < limit) of the sorted order == count of keys below limit
+      int below = 0;
+      for (const auto& e : order) below += e.second < limit ? 1 : 0;
+      min_coeffs = std::max<int>(min_coeffs, below);
+      *first_up_iter = false;
+    }
+  }
+  void Applied(float key) {
+    val_threshold = key;
+    ++changed;
+  }
+  // after change i: its decade's codes are read (rebuild them), the estimate is read
+  bool CodesRead(size_t i) const {
+    return i % 10 == 0 && (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs)) || i + 10 >= n_order);
+  }
+  bool EstimateRead(size_t i) const { return changed > min_coeffs || i + 1 == n_order; }
+  bool Stop(int est, int prev) const { return changed > min_coeffs && std::abs(est - prev) > min_size_delta; }
+};
+
 struct AcBlockModel {
   std::vector<uint64_t> nz;  // [c * blocks + b]: bit z set <=> zigzag coefficient z non-zero
   float inv_q[3][kDCTBlockSize];  // 1 / quant (natural order), for Size
@@ -1032,6 +1078,18 @@ class Processor {
                               const std::vector<float>& errors, std::string* err);
   bool GatherEntries(std::vector<std::pair<int, float>>* entries, int own_lo, int own_hi, int gbase,
                      int* blocks_to_change);
+  // The change entries of one back-end iteration (processor.cc:776-834), for
+  // both back ends: the block weights at rblock = 1..4 until some block has
+  // entries, every (owned) block's entries in block order -- built in
+  // parallel over chunks of blocks -- and on a partitioned frame the frame's
+  // entries from every rank.  factor: the searched blocks' size in 8x8
+  // blocks; bmax: their distance maxima.  False: a failed exchange.
+  bool BuildChangeOrder(int direction, int factor, double target_mul, int num_blocks, int own_lo,
+                        int own_hi, int gbase, const std::vector<float>& bmax,
+                        const std::vector<int>& last_indexes, const std::vector<int>& offsets,
+                        const std::vector<float>& cand_err, const std::vector<float>& max_block_error,
+                        std::vector<std::pair<int, float>>* order, std::vector<float>* block_weight,
+                        int* blocks_to_change);
   // The 4:2:0 pass (processor.cc:989-1016, downsample = 1) on the host model
   // Image420, entropy coded on the host.
   int Run420(const JpegData& jpg_in, std::string* err);
@@ -1186,69 +1244,11 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
       std::vector<float> block_weight;
-      for (int rblock = 1; rblock <= 4; ++rblock) {
-        block_weight.assign(num_blocks, 0.0f);
-        const std::vector<float>& bmax = first_up_iter ? zero_block_max : cmp_->block_max_distance();
-        cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, 1, 1, bmax,
-                                                 &block_weight);
-        // the candidate entries of every (owned) block in block order
-        // (processor.cc:806-829), built in parallel over chunks of blocks:
-        // entry counts, their prefix sums, then each chunk fills its own range
-        std::vector<size_t> chunk_start(own_chunks + 1, 0);
-        std::vector<int> chunk_btc(own_chunks, 0);
-        auto block_entries = [&](int bix) -> int {
-          if (block_weight[bix] == 0) return 0;
-          const int last_index = last_indexes[bix];
-          const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
-          const int num_candidates = offsets[bix + 1] - offset;
-          return direction > 0 ? std::max(0, num_candidates - last_index) : last_index;
-        };
-        ParallelFor(own_chunks, [&](int ch) {
-          size_t n = 0;
-          int btc = 0;
-          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
-            const int e = block_entries(bix);
-            n += e;
-            btc += e > 0 ? 1 : 0;
-          }
-          chunk_start[ch + 1] = n;
-          chunk_btc[ch] = btc;
-        });
-        blocks_to_change = 0;
-        for (int ch = 0; ch < own_chunks; ++ch) {
-          chunk_start[ch + 1] += chunk_start[ch];
-          blocks_to_change += chunk_btc[ch];
-        }
-        global_order.resize(chunk_start[own_chunks]);
-        ParallelFor(own_chunks, [&](int ch) {
-          std::pair<int, float>* out = global_order.data() + chunk_start[ch];
-          for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
-            if (block_weight[bix] == 0) continue;
-            const int last_index = last_indexes[bix];
-            const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand_err.size()) - 1));
-            const int num_candidates = offsets[bix + 1] - offset;
-            const float* errs = cand_err.data() + offset;
-            const float max_err = max_block_error[bix];
-            const int g = gbase + bix;
-            if (direction > 0) {
-              for (int i = last_index; i < num_candidates; ++i)
-                *out++ = std::make_pair(g, (errs[i] - max_err) / block_weight[bix]);
-            } else {
-              for (int i = last_index - 1; i >= 0; --i)
-                *out++ = std::make_pair(g, (max_err - errs[i]) / block_weight[bix]);
-            }
-          }
-        });
-        if (part_ && part_->world > 1) {
-          // the frame's order: every rank's entries in rank (= block) order;
-          // a rank sends its keys and a count per owned block
-          const auto tx = Clock::now();
-          if (!GatherEntries(&global_order, own_lo, own_hi, gbase, &blocks_to_change))
-            return exchange_failed();
-          res_->detail["strip_entries_s"] += Since(tx);
-        }
-        if (!global_order.empty()) break;
-      }
+      if (!BuildChangeOrder(direction, 1, target_mul, num_blocks, own_lo, own_hi, gbase,
+                            first_up_iter ? zero_block_max : cmp_->block_max_distance(), last_indexes,
+                            offsets, cand_err, max_block_error, &global_order, &block_weight,
+                            &blocks_to_change))
+        return exchange_failed();
       res_->detail["backend_order_s"] += Since(tb);
       res_->detail["backend_order_entries"] += static_cast<double>(global_order.size());
       if (global_order.empty()) {
@@ -1259,25 +1259,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // lazily: only the prefix the change loop consumes gets sorted.
       LazyStdSort sorter(global_order.data(), global_order.size());
       const auto tc = Clock::now();
-      double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
-      if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
-      const double min_size_delta = base_size * rel_size_delta;
-      const float per_block = direction > 0 ? 2.0f : 1 * 1 * 0.2f;
-      int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
-      if (first_up_iter) {
-        const float limit = 0.75f * cmp_->BlockErrorLimit();
-        // partition_point(key < limit) of the sorted order == count of keys below limit
-        int below = 0;
-        for (const auto& e : global_order) below += e.second < limit ? 1 : 0;
-        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, below);
-        first_up_iter = false;
-      }
-      float val_threshold = 0.0f;
-      int changed_coeffs = 0;
+      ChangeLoop loop(direction, cmp_->DistanceOK(1.0), base_size, 1, blocks_to_change, &first_up_iter,
+                      cmp_->BlockErrorLimit(), global_order);
       int est_jpg_size = prev_size;
       // Changes before the loop's first read of an entropy code or size
       // estimate (first_read: the first i % 10 == 0 step whose codes are
-      // read, the first step with changed_coeffs > min_coeffs_to_change, or
+      // read, the first step with changed > min_coeffs_to_change, or
       // the last one) only accumulate; their effect -- block states, AC
       // histograms, last_indexes -- depends on which changes they are, not
       // on their order.  So [0, first_read) is taken as std::sort's first
@@ -1285,7 +1272,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // only, no sort of the prefix) and applied per block in parallel.
       size_t bulk = 0;
       {
-        const long m = std::max(0, min_coeffs_to_change);
+        const long m = std::max(0, loop.min_coeffs);
         const long n = static_cast<long>(global_order.size());
         const long lo = std::max(0L, std::min(m - 9, n - 10));
         const long first_code = (lo + 9) / 10 * 10;
@@ -1383,14 +1370,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           for (int q = 0; q + 1 < JpegHistogram::kSize; ++q)
             ac_histograms[c].counts[q] += static_cast<uint32_t>(hsum[c * (JpegHistogram::kSize - 1) + q]);
         refresh_raw();
-        changed_coeffs = static_cast<int>(bulk);
+        loop.changed = static_cast<int>(bulk);
         res_->detail["backend_bulk_s"] += Since(tbk);
         res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
       }
-      // The size estimate only matters once changed_coeffs > min_coeffs_to_change
-      // and at the last step (it becomes prev_size); the entropy codes it uses
-      // are those of the last i % 10 == 0 step.  Codes of decades that contain
-      // no such step are never read, so they are not built.  Exact.
       const size_t n_order = global_order.size();
       double codes_s = 0.0;
       int n_codes = 0;
@@ -1398,20 +1381,17 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // one change's bookkeeping after it was applied: the decade's codes,
       // the estimate and the break test; true: stop after change i
       auto after_change = [&](size_t i) -> bool {
-        val_threshold = global_order[i].second;
-        ++changed_coeffs;
-        const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
-        if (i % 10 == 0 &&
-            (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs_to_change)) || i + 10 >= n_order)) {
+        loop.Applied(global_order[i].second);
+        if (loop.CodesRead(i)) {
           const auto te = Clock::now();
           ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
           refresh_raw();
           codes_s += Since(te);
           ++n_codes;
         }
-        if (!needed) return false;
+        if (!loop.EstimateRead(i)) return false;
         est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
-        return changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta;
+        return loop.Stop(est_jpg_size, prev_size);
       };
       // the change of the next entry of owned block bix applied to img: its
       // symbol updates into the frame's histograms, or (log) recorded
@@ -1566,8 +1546,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       res_->detail["backend_codes_s"] += codes_s;
       res_->detail["backend_sort_s"] += sort_s;
       res_->detail["backend_entropy_codes"] += n_codes;
-      res_->detail["backend_changes"] += changed_coeffs;
-      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
+      res_->detail["backend_changes"] += loop.changed;
+      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * loop.val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
@@ -1576,6 +1556,78 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
     }
   }
   FlushOutput();
+  return true;
+}
+
+bool Processor::BuildChangeOrder(int direction, int factor, double target_mul, int num_blocks,
+                                 int own_lo, int own_hi, int gbase, const std::vector<float>& bmax,
+                                 const std::vector<int>& last_indexes, const std::vector<int>& offsets,
+                                 const std::vector<float>& cand_err,
+                                 const std::vector<float>& max_block_error,
+                                 std::vector<std::pair<int, float>>* order,
+                                 std::vector<float>* block_weight, int* blocks_to_change) {
+  const int own_chunks = (own_hi - own_lo + kOrderChunk - 1) / kOrderChunk;
+  const int cand_n = static_cast<int>(cand_err.size());
+  std::vector<float>& weight = *block_weight;
+  for (int rblock = 1; rblock <= 4; ++rblock) {
+    weight.assign(num_blocks, 0.0f);
+    cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, factor, factor, bmax, &weight);
+    // entry counts per chunk of blocks, their prefix sums, then each chunk
+    // fills its own range
+    std::vector<size_t> chunk_start(own_chunks + 1, 0);
+    std::vector<int> chunk_btc(own_chunks, 0);
+    auto block_entries = [&](int bix) -> int {
+      if (weight[bix] == 0) return 0;
+      const int last_index = last_indexes[bix];
+      const int offset = std::max(0, std::min(offsets[bix], cand_n - 1));
+      const int num_candidates = offsets[bix + 1] - offset;
+      return direction > 0 ? std::max(0, num_candidates - last_index) : last_index;
+    };
+    ParallelFor(own_chunks, [&](int ch) {
+      size_t n = 0;
+      int btc = 0;
+      for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
+        const int e = block_entries(bix);
+        n += e;
+        btc += e > 0 ? 1 : 0;
+      }
+      chunk_start[ch + 1] = n;
+      chunk_btc[ch] = btc;
+    });
+    *blocks_to_change = 0;
+    for (int ch = 0; ch < own_chunks; ++ch) {
+      chunk_start[ch + 1] += chunk_start[ch];
+      *blocks_to_change += chunk_btc[ch];
+    }
+    order->resize(chunk_start[own_chunks]);
+    ParallelFor(own_chunks, [&](int ch) {
+      std::pair<int, float>* out = order->data() + chunk_start[ch];
+      for (int bix = own_lo + ch * kOrderChunk; bix < std::min(own_hi, own_lo + (ch + 1) * kOrderChunk); ++bix) {
+        if (weight[bix] == 0) continue;
+        const int last_index = last_indexes[bix];
+        const int offset = std::max(0, std::min(offsets[bix], cand_n - 1));
+        const int num_candidates = offsets[bix + 1] - offset;
+        const float* errs = cand_err.data() + offset;
+        const float max_err = max_block_error[bix];
+        const int g = gbase + bix;
+        if (direction > 0) {
+          for (int i = last_index; i < num_candidates; ++i)
+            *out++ = std::make_pair(g, (errs[i] - max_err) / weight[bix]);
+        } else {
+          for (int i = last_index - 1; i >= 0; --i)
+            *out++ = std::make_pair(g, (max_err - errs[i]) / weight[bix]);
+        }
+      }
+    });
+    if (part_ && part_->world > 1) {
+      // the frame's order: every rank's entries in rank (= block) order; a
+      // rank sends its keys and a count per owned block
+      const auto tx = Clock::now();
+      if (!GatherEntries(order, own_lo, own_hi, gbase, blocks_to_change)) return false;
+      res_->detail["strip_entries_s"] += Since(tx);
+    }
+    if (!order->empty()) break;
+  }
   return true;
 }
 
@@ -1948,7 +2000,6 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
   std::vector<int> last_indexes(num_blocks, 0);
   res_->seconds_backend += Since(tb0);
   bool first_up_iter = true;
-  const int cand_n = static_cast<int>(cand_err.size());
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early && direction == -1) {
@@ -1959,43 +2010,22 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
       std::vector<float> block_weight;
-      for (int rblock = 1; rblock <= 4; ++rblock) {
-        block_weight.assign(num_blocks, 0.0f);
-        // the distance map's maximum per searched block (all zero on the first
-        // up iteration, processor.cc:777-780)
-        std::vector<float> bmax(num_blocks, 0.0f);
-        if (!first_up_iter) {
-          const std::vector<float>& m8 = cmp_->block_max_distance();
-          const int bw8 = (w + 7) / 8, bh8 = (h + 7) / 8;
-          for (int by = 0; by < bh8; ++by)
-            for (int bx = 0; bx < bw8; ++bx) {
-              float& d = bmax[(by / factor) * block_width + bx / factor];
-              d = std::max(d, m8[by * bw8 + bx]);
-            }
-        }
-        cmp_->ComputeBlockErrorAdjustmentWeights(direction, rblock, target_mul, factor, factor, bmax,
-                                                 &block_weight);
-        global_order.clear();
-        blocks_to_change = 0;
-        for (int bix = 0; bix < num_blocks; ++bix) {
-          const int last_index = last_indexes[bix];
-          const int offset = std::max(0, std::min(offsets[bix], cand_n - 1));
-          const int num_candidates = offsets[bix + 1] - offset;
-          const float* errs = cand_err.data() + offset;
-          const float max_err = max_block_error[bix];
-          if (block_weight[bix] == 0) continue;
-          if (direction > 0) {
-            for (int i = last_index; i < num_candidates; ++i)
-              global_order.push_back(std::make_pair(bix, (errs[i] - max_err) / block_weight[bix]));
-            blocks_to_change += last_index < num_candidates ? 1 : 0;
-          } else {
-            for (int i = last_index - 1; i >= 0; --i)
-              global_order.push_back(std::make_pair(bix, (max_err - errs[i]) / block_weight[bix]));
-            blocks_to_change += last_index > 0 ? 1 : 0;
+      // the distance map's maximum per searched block (all zero on the first
+      // up iteration, processor.cc:777-780)
+      std::vector<float> bmax(num_blocks, 0.0f);
+      if (!first_up_iter) {
+        const std::vector<float>& m8 = cmp_->block_max_distance();
+        const int bw8 = (w + 7) / 8, bh8 = (h + 7) / 8;
+        for (int by = 0; by < bh8; ++by)
+          for (int bx = 0; bx < bw8; ++bx) {
+            float& d = bmax[(by / factor) * block_width + bx / factor];
+            d = std::max(d, m8[by * bw8 + bx]);
           }
-        }
-        if (!global_order.empty()) break;
       }
+      if (!BuildChangeOrder(direction, factor, target_mul, num_blocks, 0, num_blocks, 0, bmax,
+                            last_indexes, offsets, cand_err, max_block_error, &global_order,
+                            &block_weight, &blocks_to_change))
+        return Fail(err);
       if (global_order.empty()) {
         res_->seconds_backend += Since(tb);
         break;
@@ -2003,21 +2033,8 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       // std::sort(global_order) (processor.cc:825-828), materialised lazily:
       // only the prefix the change loop consumes gets sorted (host/lazy_sort.h)
       LazyStdSort sorter(global_order.data(), global_order.size());
-      double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
-      if (direction > 0 && cmp_->DistanceOK(1.0)) rel_size_delta = 0.05;
-      const double min_size_delta = base_size * rel_size_delta;
-      const float per_block = direction > 0 ? 2.0f : factor * factor * 0.2f;
-      int min_coeffs_to_change = static_cast<int>(per_block * blocks_to_change);
-      if (first_up_iter) {
-        const float limit = 0.75f * cmp_->BlockErrorLimit();
-        // partition_point(key < limit) of the sorted order == count of keys below limit
-        int below = 0;
-        for (const auto& e : global_order) below += e.second < limit ? 1 : 0;
-        min_coeffs_to_change = std::max<int>(min_coeffs_to_change, below);
-        first_up_iter = false;
-      }
-      float val_threshold = 0.0f;
-      int changed_coeffs = 0;
+      ChangeLoop loop(direction, cmp_->DistanceOK(1.0), base_size, factor, blocks_to_change,
+                      &first_up_iter, cmp_->BlockErrorLimit(), global_order);
       int est_jpg_size = prev_size;
       const size_t n_order = global_order.size();
       for (size_t i = 0; i < n_order; ++i) {
@@ -2040,24 +2057,17 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
         UpdateACHistogram(1, block, quant, &ac_histograms[c]);
         img->SetCoeffBlock(c, bix, block);
         last_indexes[bix] += direction;
-        val_threshold = global_order[i].second;
-        ++changed_coeffs;
-        // the estimate is read only once changed_coeffs > min_coeffs_to_change
-        // and at the last step; a decade's codes only if such a step reads
-        // them (as the 4:4:4 back end) -- the same values where they are read
-        const bool needed = changed_coeffs > min_coeffs_to_change || i + 1 == n_order;
-        if (i % 10 == 0 &&
-            (i + 9 >= static_cast<size_t>(std::max(0, min_coeffs_to_change)) || i + 10 >= n_order))
-          ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
-        if (!needed) continue;
+        loop.Applied(global_order[i].second);
+        if (loop.CodesRead(i)) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
+        if (!loop.EstimateRead(i)) continue;
         est_jpg_size = jpg_header_size + dc_size + ac_histogram_size +
                        static_cast<int>(EntropyCodedDataSize(ac_histograms, ac_depths));
-        if (changed_coeffs > min_coeffs_to_change && std::abs(est_jpg_size - prev_size) > min_size_delta) break;
+        if (loop.Stop(est_jpg_size, prev_size)) break;
       }
-      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * val_threshold * direction;
+      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * loop.val_threshold * direction;
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
-      res_->detail["backend420_changes"] += changed_coeffs;
+      res_->detail["backend420_changes"] += loop.changed;
       res_->seconds_backend += Since(tb);
       std::string encoded;
       {
