@@ -88,11 +88,13 @@ def stage_bytes_per_px():
     return s
 
 
-# Per-block greedy zeroing search (k_block_zeroing), per 8x8 block: reads the
-# candidate and q=1 coefficients (2 x 3 x 64 int16), the block's RGB8 pixels
-# (192 B) and its 3 mask scales; writes its 192-entry CoeffData order (8 B
-# each) and its kept-entry count.
-ZEROING_BYTES_PER_BLOCK = 384 + 384 + 192 + 12 + 192 * 8 + 4
+# Per-block greedy zeroing search (k_block_zeroing, the search's compacted
+# form), per 8x8 block: reads the candidate and q=1 coefficients (2 x 3 x 64
+# int16), the block's RGB8 pixels (192 B) and its 3 mask scales, writes its
+# kept-entry count; per kept entry (the search's candidates) one u8 index and
+# one f32 error.
+ZEROING_BYTES_PER_BLOCK = 384 + 384 + 192 + 12 + 4
+ZEROING_BYTES_PER_KEPT = 1 + 4
 
 
 # The launches of one search-loop Compare pass (each kernel once; the other
@@ -110,11 +112,12 @@ JPEG_STAGE_BYTES_PER_MCU = 3 * 64 * 2 * 2 + 3 * 8
 JPEG_CODE_BYTES_PER_MCU = 3 * 64 * 2
 
 
-def region_bytes(name, w, h):
-    """Algorithmic HBM bytes per launch of a profiled region, or None."""
+def region_bytes(name, w, h, kept=None):
+    """Algorithmic HBM bytes per launch of a profiled region, or None.
+    kept: the zeroing search's kept entries (candidates) of the frame."""
     blocks = ((w + 7) // 8) * ((h + 7) // 8)
     if name == "block_zeroing":
-        return ZEROING_BYTES_PER_BLOCK * blocks
+        return ZEROING_BYTES_PER_BLOCK * blocks + ZEROING_BYTES_PER_KEPT * (kept or 0)
     if name == "jpeg_stage":
         return JPEG_STAGE_BYTES_PER_MCU * blocks
     if name == "jpeg_code":
@@ -592,13 +595,14 @@ def main():
     value = total_px / elapsed / 1e6
 
     bpp = stage_bytes_per_px()
+    kept = int(host.get("candidates", 0))  # the single frame's kept zeroing entries
     stages = {}
     regions = []
     for name, (cnt, ms) in prof.items():
         if not cnt:
             continue
         avg = ms / cnt
-        b = region_bytes(name, w, h)
+        b = region_bytes(name, w, h, kept)
         row = {"launches": cnt, "avg_ms": round(avg, 4), "frame_ms": round(ms, 4)}
         if b is not None:
             row["algo_GBps"] = round(b / (avg * 1e-3) / 1e9, 1)
@@ -611,7 +615,7 @@ def main():
     def roof_of(name):
         cnt, ms = prof[name]
         avg = ms / cnt
-        b = region_bytes(name, w, h)
+        b = region_bytes(name, w, h, kept)
         achieved = b / (avg * 1e-3) / 1e9
         traffic, tsrc = measured_traffic(name, w, h)
         r = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),

@@ -1258,7 +1258,7 @@ bool Engine::JpegStageEnqueueRange(const int q[3][64], int m0, int m1) {
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
   // (the device counts are zero: cleared at creation, and by the last
   // workgroup of every stage after it has published them to h_jhist_)
-  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, 1024, 0, s>>>(
+  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, kStageThreads, 0, s>>>(
       d_cur_, qf, nb_, m0, m1, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;

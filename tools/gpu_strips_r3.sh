@@ -10,9 +10,3 @@ head -c 600 $O/w1.json; echo
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
   --master-port 29611 tools/strip_bench.py --warmup 1 --backend gloo --one-device > $O/w4.json 2> $O/w4.err || { tail -30 $O/w4.err; exit 1; }
 head -c 900 $O/w4.json; echo
-# the same with sleeping waits (4 processes share one GPU here: the runtime's
-# polling waits would count as host CPU of every rank)
-GZ_WAIT_SLEEP_US=50 GZ_WAIT_SPIN_US=20 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
-  --master-addr 127.0.0.1 --master-port 29612 tools/strip_bench.py --warmup 1 --backend gloo --one-device \
-  > $O/w4_sleep.json 2> $O/w4_sleep.err || { tail -30 $O/w4_sleep.err; exit 1; }
-head -c 300 $O/w4_sleep.json; echo
