@@ -867,7 +867,9 @@ struct AcBlockModel {
   // DC) through the non-zeros `mid` (0: none) and `nx` (0: none; then EOB
   // if the last one is below 63).
   // H: the histogram (JpegHistogram) or a recorder of the same Add calls.
-  template <class H>
+  // kRaw = false: the histogram only (the bulk prefix, whose raw bits are
+  // recomputed from the summed histograms)
+  template <class H, bool kRaw = true>
   static void Segment(int weight, int p, int mid, int mid_size, int nx, int nx_size,
                       const uint8_t* depth, H* h, int64_t* raw) {
     int last = p;
@@ -876,12 +878,12 @@ struct AcBlockModel {
       int run = pos - last - 1;
       while (run > 15) {
         h->Add(0xf0, weight);
-        bits += depth[0xf0];
+        if (kRaw) bits += depth[0xf0];
         run -= 16;
       }
       const int sym = (run << 4) + size;
       h->Add(sym, weight);
-      bits += depth[sym] + (sym & 0xf);
+      if (kRaw) bits += depth[sym] + (sym & 0xf);
       last = pos;
     };
     if (mid) put(mid, mid_size);
@@ -889,13 +891,13 @@ struct AcBlockModel {
       put(nx, nx_size);
     } else if (last < 63) {
       h->Add(0, weight);
-      bits += depth[0];
+      if (kRaw) bits += depth[0];
     }
-    *raw += weight * bits;
+    if (kRaw) *raw += weight * bits;
   }
 
   // block[k] := newval with the histogram / raw-bit bookkeeping.
-  template <class H>
+  template <class H, bool kRaw = true>
   void Change(int c, int bix, int blocks, coeff_t* block, int k, coeff_t newval, const int* q,
               const uint8_t* depth, H* h, int64_t* raw) {
     const coeff_t old = block[k];
@@ -909,9 +911,10 @@ struct AcBlockModel {
     const int nx = above ? __builtin_ctzll(above) : 0;
     const int knx = kJPEGNaturalOrder[nx];
     const int nx_size = nx ? SizeInv(block[knx], q[knx], inv_q[c][knx]) : 0;
-    Segment(-1, p, old ? z : 0, old ? SizeInv(old, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h, raw);
-    Segment(1, p, newval ? z : 0, newval ? SizeInv(newval, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h,
-            raw);
+    Segment<H, kRaw>(-1, p, old ? z : 0, old ? SizeInv(old, q[k], inv_q[c][k]) : 0, nx, nx_size, depth, h,
+                     raw);
+    Segment<H, kRaw>(1, p, newval ? z : 0, newval ? SizeInv(newval, q[k], inv_q[c][k]) : 0, nx, nx_size, depth,
+                     h, raw);
     if (newval) m |= 1ull << z; else m &= ~(1ull << z);
   }
 };
@@ -1342,18 +1345,24 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             --pending;
             const int bx = bix % block_width, by = bix / block_width;
             const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+            int li = last_indexes[bix];
             for (int t = 0; t < cnt; ++t) {
-              const int idx = cand[offset + last_indexes[bix] + std::min(direction, 0)];
+              const int idx = cand[offset + li + std::min(direction, 0)];
               const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
               const int* quant = img->quant[c];
-              const JpegComponent& comp = jpg.components[c];
-              const int jpg_bix = by * comp.width_in_blocks + bx;
-              const int newval = direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
-              acm.Change(c, bix, num_blocks, img->block(c, bix), k, static_cast<coeff_t>(newval), quant,
-                         &ac_depths[c * JpegHistogram::kSize], &d.h[c], &raw_unused);
+              int newval = 0;
+              if (direction < 0) {
+                const JpegComponent& comp = jpg.components[c];
+                const int jpg_bix = by * comp.width_in_blocks + bx;
+                newval = QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
+              }
+              acm.Change<JpegHistogram, false>(c, bix, num_blocks, img->block(c, bix), k,
+                                               static_cast<coeff_t>(newval), quant,
+                                               &ac_depths[c * JpegHistogram::kSize], &d.h[c], &raw_unused);
               d.changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * num_blocks + bix) * 64 + k));
-              last_indexes[bix] += direction;
+              li += direction;
             }
+            last_indexes[bix] = li;
           }
         });
         // (symbols only: the last slot is the histogram's fixed sentinel count)
