@@ -106,7 +106,7 @@ bool HipButteraugliComparator::OriginalJpegData(JpegData* jpg) {
   for (auto& q : jpg->quant)
     for (int k = 0; k < kDCTBlockSize; ++k) q.values[k] = 1;
   const size_t per = static_cast<size_t>(engine_->blocks()) * 64;
-  orig_.resize(3 * per);
+  if (orig_.size() != 3 * per) orig_.reset(3 * per);
   if (!engine_->ComputeOriginalCoeffs(orig_.data())) {
     err_ = engine_->error();
     return false;
@@ -129,11 +129,15 @@ bool HipButteraugliComparator::SetOriginalCoeffs(const JpegData& jpg) {
     if (same) return true;
   }
   orig_on_device_ = false;
-  std::vector<coeff_t>& all = orig_;
-  all.clear();
-  for (int c = 0; c < 3; ++c)
-    all.insert(all.end(), jpg.components[c].coeffs.begin(), jpg.components[c].coeffs.end());
-  if (!engine_->SetOriginalCoeffs(all.data(), false)) {
+  size_t total = 0;
+  for (int c = 0; c < 3; ++c) total += jpg.components[c].coeffs.size();
+  orig_.reset(total);
+  coeff_t* all = orig_.data();
+  for (int c = 0; c < 3; ++c) {
+    std::memcpy(all, jpg.components[c].coeffs.data(), jpg.components[c].coeffs.size() * sizeof(coeff_t));
+    all += jpg.components[c].coeffs.size();
+  }
+  if (!engine_->SetOriginalCoeffs(orig_.data(), false)) {
     err_ = engine_->error();
     return false;
   }
@@ -1725,6 +1729,9 @@ void RemoveOriginalQuantization(JpegData* jpg, int q_in[3][kDCTBlockSize]) {
     JpegComponent& c = jpg->components[i];
     const int* q = jpg->quant[c.quant_idx].values;
     std::memcpy(q_in[i], q, sizeof(q_in[i]));
+    bool ones = true;  // (RGB input: the q=1 originals -- nothing to multiply)
+    for (int k = 0; k < kDCTBlockSize; ++k) ones = ones && q[k] == 1;
+    if (ones) continue;
     for (size_t j = 0; j < c.coeffs.size(); ++j) c.coeffs[j] = static_cast<coeff_t>(c.coeffs[j] * q[j % 64]);
   }
   int ones[3][kDCTBlockSize];

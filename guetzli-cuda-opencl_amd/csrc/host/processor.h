@@ -222,7 +222,19 @@ class HipButteraugliComparator : public Comparator {
                             bool strip_metadata, size_t* size);
 
   std::unique_ptr<Engine> engine_;
-  std::vector<coeff_t> orig_;      // q=1 coefficients of the original (host copy)
+  // q=1 coefficients of the original (host copy; 12 MB at 1080p, allocated
+  // without the zero fill a std::vector would write first)
+  struct CoeffBuffer {
+    std::unique_ptr<coeff_t[]> p;
+    size_t n = 0;
+    void reset(size_t count) {
+      if (count != n) p.reset(new coeff_t[count]);
+      n = count;
+    }
+    size_t size() const { return n; }
+    coeff_t* data() { return p.get(); }
+    const coeff_t* data() const { return p.get(); }
+  } orig_;
   bool orig_on_device_ = false;
   std::vector<coeff_t> delta_val_;
   int w_ = 0, h_ = 0;
