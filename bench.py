@@ -467,6 +467,10 @@ def main():
                     help="frames per GPU per step, encoded concurrently")
     ap.add_argument("--in-flight", type=int, default=0,
                     help="frames encoded at once per GPU (0: all frames of the step)")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="start a step's frames only after the previous step's last frame "
+                         "finished (default: the timed steps' frames go through one queue, "
+                         "--in-flight at a time, so a frame starts when any frame finishes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-processes", type=int, default=8)
     ap.add_argument("--no-large-frame", action="store_true",
@@ -515,8 +519,11 @@ def main():
     def encode(t):
         return gz.process_device(t.data_ptr(), w, h, params, device=dev, return_stats=True)
 
-    def step(s):
-        res = list(pool.map(encode, frames[s]))
+    def submit(s):
+        return [pool.submit(encode, t) for t in frames[s]]
+
+    def step(s, futs=None):
+        res = [f.result() for f in (futs if futs is not None else submit(s))]
         out = [r[0] for r in res]
         if dist is not None:
             # the final gather of the JPEG byte strings over RCCL/xGMI
@@ -538,8 +545,14 @@ def main():
     checked = []
     keys = ("seconds_total", "seconds_setup", "seconds_write", "seconds_quantize",
             "seconds_backend", "seconds_compare", "seconds_zeroing")
+    # Streaming (default): every timed frame is queued at once and the pool
+    # keeps in_flight of them encoding, so the steps' frames overlap at step
+    # boundaries (no per-step tail, no frames entering their host-heavy
+    # phases together); each step's outputs are gathered once its frames are
+    # done.  --lockstep: a step starts when the previous one has finished.
+    futs = {} if args.lockstep else {s: submit(s) for s in range(args.warmup, nsteps)}
     for s in range(args.warmup, nsteps):
-        out, stats = step(s)
+        out, stats = step(s, futs.get(s))
         if s == args.warmup:
             checked = [(seeds[s][f], out[f], stats[f].iterations)
                        for f in range(len(out)) if seeds[s][f] in kn]
@@ -681,6 +694,8 @@ def main():
                    "width": w, "height": h, "quality": q,
                    "frames_per_gpu_per_step": args.frames_per_step,
                    "frames_in_flight": in_flight,
+                   "schedule": "lockstep steps" if args.lockstep else
+                               "one queue over the timed steps' frames",
                    "parallelism": "image-sharded over %d GPU(s)%s" % (
                        world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
                    "search_iterations": iters},
