@@ -128,6 +128,13 @@ void BuildTables(GzTables* t) {
     t->block_csf[i] = static_cast<float>(kBlockCsfD[i]);
     t->block_csf_d[i] = kBlockCsfD[i];
   }
+  // the AC sums' term csf_d[k] * 64.8 * sq[k] is (csf_d[k] * 64.8) * sq[k]:
+  // its first product per k, formed here with the same double multiply
+  for (int k = 4; k < 37; ++k) {
+    t->ac_w_d[0][k - 4] = kBlockCsfD[k] * 64.8;
+    t->ac_w_d[1][k - 4] = 1.0;  // Y: acc += t1[k] == acc += 1.0 * t1[k]
+    t->ac_w_d[2][k - 4] = kBlockCsfD[k] * 2.4;
+  }
   memcpy(t->zeroing_csf, kZeroingCsf, sizeof(kZeroingCsf));
   {
     static const uint8_t kZigZag[64] = {
