@@ -712,6 +712,9 @@ def main():
         "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
         "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
         "host_cores_busy_per_gpu": round(cpu_s / elapsed, 2),
+        "host_cpu_user_system_seconds_per_frame": [
+            round((ru1.ru_utime - ru0.ru_utime) / (args.steps * args.frames_per_step), 4),
+            round((ru1.ru_stime - ru0.ru_stime) / (args.steps * args.frames_per_step), 4)],
         "single_frame": {"seconds": round(single_s, 4),
                          "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
                          "iterations": st1.iterations,

@@ -51,15 +51,19 @@ class Pool {
     job.fn = &fn;
     job.n = n;
     std::list<Job*>::iterator it;
+    int wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       it = jobs_.insert(jobs_.end(), &job);
+      // wake as many workers as there are items for them (the caller takes
+      // one), and no more than are asleep and not already being woken: with
+      // several frames in flight most workers are busy on other frames'
+      // jobs and take this one's items when they finish theirs, so waking
+      // more only costs futex calls and futile wake-ups (the pool's system
+      // time)
+      wake = std::max(0, std::min(n - 1, idle_ - signaled_));
+      signaled_ += wake;
     }
-    // wake as many workers as there are items for them (the caller takes
-    // one): a notify_all per call would wake every idle worker of the
-    // process for each of the hundreds of small passes a frame makes, most
-    // of them only to find nothing left and sleep again
-    const int wake = std::min(n - 1, static_cast<int>(threads_.size()));
     for (int i = 0; i < wake; ++i) cv_.notify_one();
     Work(&job);
     {
@@ -102,14 +106,18 @@ class Pool {
       int i;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] {
+        for (;;) {
           for (Job* j : jobs_)
             if (j->next.load() < j->n) {
               job = j;
-              return true;
+              break;
             }
-          return false;
-        });
+          if (job) break;
+          ++idle_;
+          cv_.wait(lk);
+          --idle_;
+          if (signaled_ > 0) --signaled_;  // (a spurious wake-up may take another's: harmless)
+        }
         // claimed under mu_: the owner erases the job under mu_ first
         i = job->next.fetch_add(1);
         if (i >= job->n) continue;
@@ -122,6 +130,8 @@ class Pool {
   std::mutex mu_;
   std::condition_variable cv_;
   std::list<Job*> jobs_;
+  int idle_ = 0;      // workers waiting on cv_ (under mu_)
+  int signaled_ = 0;  // of those, already notified and not yet awake
 };
 
 Pool* GetPool() {
