@@ -465,8 +465,12 @@ def main():
     ap.add_argument("--quality", type=int, default=95)
     ap.add_argument("--frames-per-step", type=int, default=8,
                     help="frames per GPU per step, encoded concurrently")
-    ap.add_argument("--in-flight", type=int, default=0,
-                    help="frames encoded at once per GPU (0: all frames of the step)")
+    ap.add_argument("--in-flight", type=int, default=10,
+                    help="frames encoded at once per GPU (0: the frames of one step)")
+    ap.add_argument("--host-threads", type=int, default=0,
+                    help="host pool threads per process, caller included (sets GZ_HOST_THREADS "
+                         "unless that is set; 0: the library's default, min(16, usable CPUs); "
+                         "the pool runs at most that minus the encodes in progress at once)")
     ap.add_argument("--lockstep", action="store_true",
                     help="start a step's frames only after the previous step's last frame "
                          "finished (default: the timed steps' frames go through one queue, "
@@ -486,6 +490,8 @@ def main():
     if args.dist_selftest:
         return dist_selftest(args)
     world, rank, local, dist = dist_setup(args.gpus)
+    if args.host_threads > 0:
+        os.environ.setdefault("GZ_HOST_THREADS", str(args.host_threads))
     import hashlib
     import torch
     import guetzli_amd as gz
@@ -694,6 +700,7 @@ def main():
                    "width": w, "height": h, "quality": q,
                    "frames_per_gpu_per_step": args.frames_per_step,
                    "frames_in_flight": in_flight,
+                   "host_pool_threads": int(os.environ.get("GZ_HOST_THREADS", "0")) or "library default",
                    "schedule": "lockstep steps" if args.lockstep else
                                "one queue over the timed steps' frames",
                    "parallelism": "image-sharded over %d GPU(s)%s" % (

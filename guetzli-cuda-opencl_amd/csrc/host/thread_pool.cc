@@ -21,6 +21,14 @@ namespace gz {
 
 namespace {
 
+std::atomic<int> g_active_encodes{0};
+
+// Workers that may run items at once: the CPUs not taken by the encodes'
+// own threads (at least one).
+int WorkerCap() {
+  return std::max(1, HostThreads() - std::max(1, g_active_encodes.load(std::memory_order_relaxed)));
+}
+
 // Several encodes (frames) run concurrently per process, each issuing its
 // own data-parallel passes: every ParallelFor is a job on a shared list and
 // idle workers take items from the oldest job that has some left, so
@@ -61,7 +69,7 @@ class Pool {
       // jobs and take this one's items when they finish theirs, so waking
       // more only costs futex calls and futile wake-ups (the pool's system
       // time)
-      wake = std::max(0, std::min(n - 1, idle_ - signaled_));
+      wake = std::max(0, std::min(std::min(n - 1, idle_ - signaled_), WorkerCap() - busy_ - signaled_));
       signaled_ += wake;
     }
     for (int i = 0; i < wake; ++i) cv_.notify_one();
@@ -107,11 +115,12 @@ class Pool {
       {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-          for (Job* j : jobs_)
-            if (j->next.load() < j->n) {
-              job = j;
-              break;
-            }
+          if (busy_ < WorkerCap())
+            for (Job* j : jobs_)
+              if (j->next.load() < j->n) {
+                job = j;
+                break;
+              }
           if (job) break;
           ++idle_;
           cv_.wait(lk);
@@ -121,8 +130,11 @@ class Pool {
         // claimed under mu_: the owner erases the job under mu_ first
         i = job->next.fetch_add(1);
         if (i >= job->n) continue;
+        ++busy_;
       }
       Drain(job, i);
+      std::lock_guard<std::mutex> lk(mu_);
+      --busy_;
     }
   }
 
@@ -131,6 +143,7 @@ class Pool {
   std::condition_variable cv_;
   std::list<Job*> jobs_;
   int idle_ = 0;      // workers waiting on cv_ (under mu_)
+  int busy_ = 0;      // workers running items (under mu_)
   int signaled_ = 0;  // of those, already notified and not yet awake
 };
 
@@ -166,6 +179,9 @@ int UsableCpus(bool* pinned) {
   return std::max(1, n);
 }
 }  // namespace
+
+ActiveEncode::ActiveEncode() { g_active_encodes.fetch_add(1, std::memory_order_relaxed); }
+ActiveEncode::~ActiveEncode() { g_active_encodes.fetch_sub(1, std::memory_order_relaxed); }
 
 int HostThreads() {
   static const int n = [] {
