@@ -565,6 +565,48 @@ bool HipButteraugliComparator::BlockZeroingCandidates420(Image420* img, int comp
   return true;
 }
 
+bool HipButteraugliComparator::DeviceOrderReset() {
+  if (!engine_->HasOrderCandidates()) return false;
+  if (!engine_->OrderReset()) {
+    err_ = engine_->error();
+    return false;
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceChangeOrder(int direction, double target_mul, bool zero_bmax,
+                                                 const std::vector<int>& last_indexes,
+                                                 std::vector<std::pair<int, float>>* order,
+                                                 int* blocks_to_change) {
+  // (ComputeBlockErrorAdjustmentWeights' target distance: target * target_mul
+  // in double, butteraugli_comparator.cc:175)
+  const double td = target_ * target_mul;
+  for (int rblock = 1; rblock <= 4; ++rblock) {
+    size_t n = 0;
+    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, &n, blocks_to_change)) {
+      err_ = engine_->error();
+      return false;
+    }
+    order->resize(n);
+    if (n) {
+      if (!engine_->OrderFetch(order->data(), n)) {
+        err_ = engine_->error();
+        return false;
+      }
+      break;
+    }
+  }
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceOrderAdvance(float val_threshold, int direction) {
+  if (!engine_->OrderAdvance(val_threshold, direction)) {
+    err_ = engine_->error();
+    return false;
+  }
+  return true;
+}
+
 double HipButteraugliComparator::ScoreOutputSize(int size) const {
   return ScoreJPEG(distance_, size, target_);
 }
@@ -1243,6 +1285,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   const std::vector<float> zero_block_max(num_blocks, 0.0f);
   bool first_up_iter = true;
   const int own_chunks = (own_hi - own_lo + kOrderChunk - 1) / kOrderChunk;
+  // the change order on the device (weights, entries, max_block_error there;
+  // the frame's candidates and block maxima are resident) unless the frame
+  // is split over ranks or the comparator has no device
+  const bool device_order = !part_ && cmp_->DeviceOrderReset();
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early) FlushOutput();  // best_size_ must be current
@@ -1251,11 +1297,16 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
       std::vector<float> block_weight;
-      if (!BuildChangeOrder(direction, 1, target_mul, num_blocks, own_lo, own_hi, gbase,
-                            first_up_iter ? zero_block_max : cmp_->block_max_distance(), last_indexes,
-                            offsets, cand_err, max_block_error, &global_order, &block_weight,
-                            &blocks_to_change))
+      if (device_order) {
+        if (!cmp_->DeviceChangeOrder(direction, target_mul, first_up_iter, last_indexes, &global_order,
+                                     &blocks_to_change))
+          return Fail(err);
+      } else if (!BuildChangeOrder(direction, 1, target_mul, num_blocks, own_lo, own_hi, gbase,
+                                   first_up_iter ? zero_block_max : cmp_->block_max_distance(), last_indexes,
+                                   offsets, cand_err, max_block_error, &global_order, &block_weight,
+                                   &blocks_to_change)) {
         return exchange_failed();
+      }
       res_->detail["backend_order_s"] += Since(tb);
       res_->detail["backend_order_entries"] += static_cast<double>(global_order.size());
       if (global_order.empty()) {
@@ -1560,7 +1611,11 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       res_->detail["backend_sort_s"] += sort_s;
       res_->detail["backend_entropy_codes"] += n_codes;
       res_->detail["backend_changes"] += loop.changed;
-      for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * loop.val_threshold * direction;
+      if (device_order) {
+        if (!cmp_->DeviceOrderAdvance(loop.val_threshold, direction)) return Fail(err);
+      } else {
+        for (int i = 0; i < num_blocks; ++i) max_block_error[i] += block_weight[i] * loop.val_threshold * direction;
+      }
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
@@ -2120,6 +2175,7 @@ int ProcessJpegData(const ProcessParams& params, const JpegData& jpg, Comparator
     if (err) *err = "4:2:0 output of a strip-decomposed frame is not supported";
     return GZ_ERR_UNSUPPORTED;
   }
+  ActiveEncode active;  // (the host pool's worker cap)
   Processor proc(params, cmp, result, cmp ? part : nullptr);
   return proc.Run(jpg, err);
 }

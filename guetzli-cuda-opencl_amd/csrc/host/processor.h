@@ -99,6 +99,20 @@ class Comparator {
                                                   double target_mul, int factor_x, int factor_y,
                                                   const std::vector<float>& max_dist_per_block,
                                                   std::vector<float>* block_weight) = 0;
+  // The 4:4:4 back end's change order built where the candidates of the
+  // last BlockZeroingCandidates and the last Compare's block maxima are (the
+  // device): DeviceOrderReset before an iteration loop (max_block_error :=
+  // 0), DeviceChangeOrder per iteration (the weights at radius 1..4 until
+  // some block has entries; the entries in block order, as
+  // Processor::BuildChangeOrder makes them), DeviceOrderAdvance after it.
+  // False from DeviceOrderReset: not available, build on the host.
+  virtual bool DeviceOrderReset() { return false; }
+  virtual bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax,
+                                 const std::vector<int>& last_indexes,
+                                 std::vector<std::pair<int, float>>* order, int* blocks_to_change) {
+    return false;
+  }
+  virtual bool DeviceOrderAdvance(float val_threshold, int direction) { return false; }
   // Makes the q=1 coefficients of the original image available to
   // QuantizeFromOriginal / BlockZeroingOrders.
   virtual bool SetOriginalCoeffs(const JpegData& jpg) = 0;
@@ -197,6 +211,10 @@ class HipButteraugliComparator : public Comparator {
                                           const std::vector<float>& max_dist_per_block,
                                           std::vector<float>* block_weight) override;
   const std::string& error() const override { return err_; }
+  bool DeviceOrderReset() override;
+  bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
+                         std::vector<std::pair<int, float>>* order, int* blocks_to_change) override;
+  bool DeviceOrderAdvance(float val_threshold, int direction) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   bool SetOriginalCoeffs420(const JpegData& jpg420) override;
   bool Compare420(const Image420& img) override;

@@ -33,6 +33,7 @@ __constant__ GzTables c_tab;
 #include "block_zeroing420.inc"
 #include "coeff_kernels.inc"
 #include "jpeg_kernels.inc"
+#include "order_kernels.inc"
 
 namespace gz {
 
@@ -604,7 +605,8 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_,
+                  d_ord_entries_};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (void* g : compare_graph_)
@@ -620,6 +622,8 @@ Engine::~Engine() {
   if (h_cand_idx_) hipHostFree(h_cand_idx_);
   if (h_cand_err_) hipHostFree(h_cand_err_);
   if (h_delta_val_) hipHostFree(h_delta_val_);
+  if (h_ord_) hipHostFree(h_ord_);
+  if (h_ord_entries_) hipHostFree(h_ord_entries_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
 
@@ -1108,6 +1112,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
                                 CoeffDataHost* out) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  ord_cand_n_ = -1;
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
   if (!OrderBlocks(comp_mask)) return false;
   long long* tr = BzTraceBuf(nb_, stream_);
@@ -1136,7 +1141,9 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
                                      static_cast<CoeffData*>(d_zero_out_), d_zero_count_, d_zero_order_,
                                      nullptr, tr, 1));
   BzTraceDump(tr, nb_, stream_);
-  return CompactCandidates(nb_, limit, offsets, idx, err, true);
+  if (!CompactCandidates(nb_, limit, offsets, idx, err, true)) return false;
+  ord_cand_n_ = static_cast<int>(err->size());  // (the device change order may use them)
+  return true;
 }
 
 // The kept entries of the first nblocks blocks' orders (d_zero_out_ /
@@ -1144,6 +1151,7 @@ bool Engine::BlockZeroingCandidates(int comp_mask, float limit, int lookahead, b
 bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offsets,
                                std::vector<uint8_t>* idx, std::vector<float>* err, bool slots) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
+  ord_cand_n_ = -1;
   if (!ScanCounts(d_zero_count_, nblocks, d_zero_off_, "scan_counts")) return false;
   if (slots) {
     GZ_TIMED("compact_candidates", k_compact_slots<<<(nblocks + 3) / 4, 256, 0, s>>>(
@@ -1176,6 +1184,125 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
   offsets->assign(h_zero_off_, h_zero_off_ + nblocks + 1);
   idx->assign(h_cand_idx_, h_cand_idx_ + total);
   err->assign(h_cand_err_, h_cand_err_ + total);
+  return true;
+}
+
+// ---- the back end's change order (order_kernels.inc) ----
+namespace {
+struct OrdLayout {
+  size_t weight, active, cnt, off, mbe, last, info, bytes;
+  explicit OrdLayout(int nb) {
+    const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
+    weight = 0;
+    active = a;
+    cnt = 2 * a;
+    off = 3 * a;
+    mbe = off + ((n + 1) * 4 + 255) / 256 * 256;
+    last = mbe + a;
+    info = last + a;
+    bytes = info + 256;
+  }
+};
+}  // namespace
+
+bool Engine::OrderReset() {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  const OrdLayout L(nb_);
+  if (!d_ord_) {
+    GZ_HIP(hipMalloc(&d_ord_, L.bytes));
+    bytes_ += L.bytes;
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ord_), static_cast<size_t>(nb_) * 4 + 64));
+  }
+  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
+  return true;
+}
+
+bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
+                        const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderBuild without candidates", 0);
+  if (static_cast<int>(last_indexes.size()) != nb_ || rblock < 1 || rblock > 4)
+    return Fail("OrderBuild arguments", 0);
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  float* weight = reinterpret_cast<float*>(base + L.weight);
+  int* active = reinterpret_cast<int*>(base + L.active);
+  int* cnt = reinterpret_cast<int*>(base + L.cnt);
+  int* off = reinterpret_cast<int*>(base + L.off);
+  int* last = reinterpret_cast<int*>(base + L.last);
+  int* info = reinterpret_cast<int*>(base + L.info);
+  const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
+  // last_indexes change between iterations only: uploaded at the first radius
+  if (rblock == 1) {
+    memcpy(h_ord_, last_indexes.data(), static_cast<size_t>(nb_) * 4);
+    GZ_HIP(hipMemcpyAsync(last, h_ord_, static_cast<size_t>(nb_) * 4, hipMemcpyHostToDevice, s));
+  }
+  GZ_HIP(hipMemsetAsync(info, 0, 16, s));
+  GZ_TIMED("order_build", k_order_local<<<groups, 256, 0, s>>>(d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock,
+                                                                target_distance, direction, weight, active));
+  if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight));
+  GZ_TIMED("order_build", k_order_counts<<<groups, 256, 0, s>>>(weight, last, d_zero_off_, ord_cand_n_, direction,
+                                                                 nb_, cnt, info));
+  if (!ScanCounts(cnt, nb_, off, "order_scan")) return false;
+  // (the staging's last_indexes copy has reached the device before these:
+  // same stream, earlier)
+  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_, off + nb_, 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_ + 1, info, 4, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  *n_entries = static_cast<size_t>(h_ord_[nb_]);
+  *blocks_to_change = h_ord_[nb_ + 1];
+  ord_direction_ = direction;
+  return true;
+}
+
+bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
+  static_assert(sizeof(OrderEntry) == sizeof(std::pair<int, float>), "entry layout");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!n) return true;
+  const size_t bytes = n * sizeof(OrderEntry);
+  if (bytes > ord_entries_cap_) {
+    if (d_ord_entries_) GZ_HIP(hipFree(d_ord_entries_));
+    d_ord_entries_ = nullptr;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    GZ_HIP(hipMalloc(&d_ord_entries_, cap));
+    ord_entries_cap_ = cap;
+  }
+  if (bytes > h_ord_entries_cap_) {
+    if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
+    h_ord_entries_ = nullptr;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap));
+    h_ord_entries_cap_ = cap;
+  }
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
+  GZ_TIMED("order_fill", k_order_fill<<<groups, 256, 0, s>>>(
+      reinterpret_cast<const float*>(base + L.weight), reinterpret_cast<const int*>(base + L.last), d_zero_off_,
+      ord_cand_n_, d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), ord_direction_, nb_,
+      reinterpret_cast<const int*>(base + L.off), static_cast<OrderEntry*>(d_ord_entries_)));
+  GZ_HIP(hipGetLastError());
+  GZ_HIP(hipMemcpyAsync(h_ord_entries_, d_ord_entries_, bytes, hipMemcpyDeviceToHost, s));
+  GZ_HIP(hipStreamSynchronize(s));
+  ProfFlush();
+  memcpy(static_cast<void*>(out), h_ord_entries_, bytes);
+  return true;
+}
+
+bool Engine::OrderAdvance(float val_threshold, int direction) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (!d_ord_) return Fail("OrderAdvance without OrderReset", 0);
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  GZ_TIMED("order_advance", k_order_advance<<<(nb_ + 255) / 256, 256, 0, s>>>(
+      reinterpret_cast<const float*>(base + L.weight), val_threshold, direction, nb_,
+      reinterpret_cast<float*>(base + L.mbe)));
+  GZ_HIP(hipGetLastError());
   return true;
 }
 

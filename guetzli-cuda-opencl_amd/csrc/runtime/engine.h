@@ -187,6 +187,22 @@ class Engine {
   bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
   bool OrderBlocks(int comp_mask);
 
+  // The search back end's change order on the device (SelectFrequencyBackEnd,
+  // processor.cc:776-834, 4:4:4 whole frame) over the candidates of the last
+  // BlockZeroingCandidates (HasOrderCandidates) and the block maxima of the
+  // last Compare.  OrderReset zeroes max_block_error; OrderBuild computes the
+  // weights at radius rblock (zero_bmax: every block maximum taken as 0),
+  // the entry counts and offsets from last_indexes (host state, uploaded)
+  // and returns their total and the blocks with entries; OrderFetch fills and
+  // downloads the n entries (block, key) in block order; OrderAdvance adds
+  // weight * val_threshold * direction to max_block_error.
+  bool HasOrderCandidates() const { return ord_cand_n_ >= 0; }
+  bool OrderReset();
+  bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
+                  const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change);
+  bool OrderFetch(std::pair<int, float>* out, size_t n);
+  bool OrderAdvance(float val_threshold, int direction);
+
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
   double last_kernel_ms(const char* which) const;
@@ -290,6 +306,18 @@ class Engine {
   int scale_stride_ = 0;
   // pinned host staging
   float* h_block_max_ = nullptr;
+  // device change order (allocated on first use): weight f32 | active i32 |
+  // counts i32 | offsets i32 [nb + 1] | max_block_error f32 | last_indexes
+  // i32 | info i32 [4]; entries; pinned staging of last_indexes + info and
+  // of the entries
+  int ord_cand_n_ = -1;             // candidates of the last 4:4:4 zeroing search (-1: none)
+  int ord_direction_ = 0;
+  void* d_ord_ = nullptr;
+  void* d_ord_entries_ = nullptr;
+  size_t ord_entries_cap_ = 0;
+  int* h_ord_ = nullptr;
+  void* h_ord_entries_ = nullptr;
+  size_t h_ord_entries_cap_ = 0;
 };
 
 // Process-wide pool of idle engines keyed by (device, width, height): an
