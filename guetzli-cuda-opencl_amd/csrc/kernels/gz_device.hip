@@ -1190,17 +1190,17 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 // ---- the back end's change order (order_kernels.inc) ----
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, mbe, last, info, bytes;
+  size_t weight, active, cnt, off, info, mbe, last, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
     active = a;
     cnt = 2 * a;
     off = 3 * a;
-    mbe = off + ((n + 1) * 4 + 255) / 256 * 256;
+    info = off + ((n + 1) * 4 + 255) / 256 * 256;  // 8 ints: per radius blocks with entries, entries
+    mbe = info + 256;
     last = mbe + a;
-    info = last + a;
-    bytes = info + 256;
+    bytes = last + a;
   }
 };
 }  // namespace
@@ -1214,7 +1214,9 @@ bool Engine::OrderReset() {
     bytes_ += L.bytes;
     GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ord_), static_cast<size_t>(nb_) * 4 + 64));
   }
-  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
+  // totals and max_block_error (adjacent) to zero
+  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.info, 0, 256 + static_cast<size_t>(nb_) * 4, s));
+  ord_adv_dir_ = 0;
   return true;
 }
 
@@ -1229,31 +1231,29 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   char* base = static_cast<char*>(d_ord_);
   float* weight = reinterpret_cast<float*>(base + L.weight);
   int* active = reinterpret_cast<int*>(base + L.active);
-  int* cnt = reinterpret_cast<int*>(base + L.cnt);
-  int* off = reinterpret_cast<int*>(base + L.off);
   int* last = reinterpret_cast<int*>(base + L.last);
   int* info = reinterpret_cast<int*>(base + L.info);
+  const OrderArgs a{last, d_zero_off_, ord_cand_n_, direction, reinterpret_cast<int*>(base + L.cnt), info};
   const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
-  // last_indexes change between iterations only: uploaded at the first radius
+  int adv_dir = 0;
   if (rblock == 1) {
+    // last_indexes change between iterations only: uploaded at the first
+    // radius, where the previous iteration's max_block_error update runs too
     memcpy(h_ord_, last_indexes.data(), static_cast<size_t>(nb_) * 4);
     GZ_HIP(hipMemcpyAsync(last, h_ord_, static_cast<size_t>(nb_) * 4, hipMemcpyHostToDevice, s));
+    adv_dir = ord_adv_dir_;
+    ord_adv_dir_ = 0;
   }
-  GZ_HIP(hipMemsetAsync(info, 0, 16, s));
   GZ_TIMED("order_build", k_order_local<<<groups, 256, 0, s>>>(d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock,
-                                                                target_distance, direction, weight, active));
-  if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight));
-  GZ_TIMED("order_build", k_order_counts<<<groups, 256, 0, s>>>(weight, last, d_zero_off_, ord_cand_n_, direction,
-                                                                 nb_, cnt, info));
-  if (!ScanCounts(cnt, nb_, off, "order_scan")) return false;
-  // (the staging's last_indexes copy has reached the device before these:
-  // same stream, earlier)
-  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_, off + nb_, 4, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_ + 1, info, 4, hipMemcpyDeviceToHost, s));
+                                                                target_distance, weight, active,
+                                                                reinterpret_cast<float*>(base + L.mbe),
+                                                                ord_adv_vt_, adv_dir, a));
+  if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
+  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_, info, 32, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
-  *n_entries = static_cast<size_t>(h_ord_[nb_]);
-  *blocks_to_change = h_ord_[nb_ + 1];
+  *blocks_to_change = h_ord_[nb_ + rblock - 1];
+  *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
   ord_direction_ = direction;
   return true;
 }
@@ -1280,12 +1280,14 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   }
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
-  const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
-  GZ_TIMED("order_fill", k_order_fill<<<groups, 256, 0, s>>>(
-      reinterpret_cast<const float*>(base + L.weight), reinterpret_cast<const int*>(base + L.last), d_zero_off_,
-      ord_cand_n_, d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), ord_direction_, nb_,
-      reinterpret_cast<const int*>(base + L.off), static_cast<OrderEntry*>(d_ord_entries_)));
-  GZ_HIP(hipGetLastError());
+  int* cnt = reinterpret_cast<int*>(base + L.cnt);
+  int* off = reinterpret_cast<int*>(base + L.off);
+  const OrderArgs a{reinterpret_cast<const int*>(base + L.last), d_zero_off_, ord_cand_n_, ord_direction_, cnt,
+                    reinterpret_cast<int*>(base + L.info)};
+  if (!ScanCounts(cnt, nb_, off, "order_scan")) return false;
+  GZ_TIMED("order_fill", k_order_fill<<<(nb_ + 255) / 256, 256, 0, s>>>(
+      reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
+      off, static_cast<OrderEntry*>(d_ord_entries_), a));
   GZ_HIP(hipMemcpyAsync(h_ord_entries_, d_ord_entries_, bytes, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
@@ -1293,16 +1295,12 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   return true;
 }
 
+// (applied by the next OrderBuild's first radius, before it overwrites the
+// weights)
 bool Engine::OrderAdvance(float val_threshold, int direction) {
-  hipStream_t s = static_cast<hipStream_t>(stream_);
-  GZ_HIP(hipSetDevice(device_));
   if (!d_ord_) return Fail("OrderAdvance without OrderReset", 0);
-  const OrdLayout L(nb_);
-  char* base = static_cast<char*>(d_ord_);
-  GZ_TIMED("order_advance", k_order_advance<<<(nb_ + 255) / 256, 256, 0, s>>>(
-      reinterpret_cast<const float*>(base + L.weight), val_threshold, direction, nb_,
-      reinterpret_cast<float*>(base + L.mbe)));
-  GZ_HIP(hipGetLastError());
+  ord_adv_vt_ = val_threshold;
+  ord_adv_dir_ = direction;
   return true;
 }
 

@@ -195,7 +195,8 @@ class Engine {
   // the entry counts and offsets from last_indexes (host state, uploaded)
   // and returns their total and the blocks with entries; OrderFetch fills and
   // downloads the n entries (block, key) in block order; OrderAdvance adds
-  // weight * val_threshold * direction to max_block_error.
+  // weight * val_threshold * direction to max_block_error (applied by the
+  // next OrderBuild, ahead of its weights).
   bool HasOrderCandidates() const { return ord_cand_n_ >= 0; }
   bool OrderReset();
   bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
@@ -307,11 +308,13 @@ class Engine {
   // pinned host staging
   float* h_block_max_ = nullptr;
   // device change order (allocated on first use): weight f32 | active i32 |
-  // counts i32 | offsets i32 [nb + 1] | max_block_error f32 | last_indexes
-  // i32 | info i32 [4]; entries; pinned staging of last_indexes + info and
+  // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | max_block_error f32
+  // | last_indexes i32; entries; pinned staging of last_indexes + totals and
   // of the entries
   int ord_cand_n_ = -1;             // candidates of the last 4:4:4 zeroing search (-1: none)
   int ord_direction_ = 0;
+  float ord_adv_vt_ = 0.0f;         // pending max_block_error update (OrderAdvance)
+  int ord_adv_dir_ = 0;
   void* d_ord_ = nullptr;
   void* d_ord_entries_ = nullptr;
   size_t ord_entries_cap_ = 0;
