@@ -693,10 +693,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": "%d concurrent synthetic %dx%d sRGB frames per GPU per step, "
-                               "q=%d, guetzli::Process end to end (each frame = BASELINE "
+        "config": {"workload": "%d synthetic %dx%d sRGB frames per GPU per step, %d encoding "
+                               "at once, q=%d, guetzli::Process end to end (each frame = BASELINE "
                                "configs[1]; 8 per GPU = configs[3]'s per-GPU share)" % (
-                                   args.frames_per_step, w, h, q),
+                                   args.frames_per_step, w, h, in_flight, q),
                    "width": w, "height": h, "quality": q,
                    "frames_per_gpu_per_step": args.frames_per_step,
                    "frames_in_flight": in_flight,
