@@ -605,8 +605,7 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
                   d_jmask_, d_jhist_, d_jcodes_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_,
-                  d_ord_entries_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (void* g : compare_graph_)
@@ -1188,9 +1187,13 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 }
 
 // ---- the back end's change order (order_kernels.inc) ----
+// Host <-> device traffic through mapped pinned memory (no copy launches):
+// the kernels read last_indexes from h_ord_ and write the totals after it
+// and the entries into h_ord_entries_; the host reads them after the
+// stream synchronisation.
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, info, mbe, last, bytes;
+  size_t weight, active, cnt, off, info, arr, mbe, last, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
@@ -1198,7 +1201,8 @@ struct OrdLayout {
     cnt = 2 * a;
     off = 3 * a;
     info = off + ((n + 1) * 4 + 255) / 256 * 256;  // 8 ints: per radius blocks with entries, entries
-    mbe = info + 256;
+    arr = info + 256;                               // arrival counters: 1 + groups / 64 + 1
+    mbe = arr + ((n / 256 / 64 + 2) * 4 + 255) / 256 * 256;
     last = mbe + a;
     bytes = last + a;
   }
@@ -1212,10 +1216,12 @@ bool Engine::OrderReset() {
   if (!d_ord_) {
     GZ_HIP(hipMalloc(&d_ord_, L.bytes));
     bytes_ += L.bytes;
-    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ord_), static_cast<size_t>(nb_) * 4 + 64));
+    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ord_), static_cast<size_t>(nb_) * 4 + 64,
+                         hipHostMallocCoherent));
+    GZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_ord_), h_ord_, 0));
+    GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.info, 0, L.mbe - L.info, s));  // totals, arrivals
   }
-  // totals and max_block_error (adjacent) to zero
-  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.info, 0, 256 + static_cast<size_t>(nb_) * 4, s));
+  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
   ord_adv_dir_ = 0;
   return true;
 }
@@ -1231,25 +1237,25 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   char* base = static_cast<char*>(d_ord_);
   float* weight = reinterpret_cast<float*>(base + L.weight);
   int* active = reinterpret_cast<int*>(base + L.active);
-  int* last = reinterpret_cast<int*>(base + L.last);
-  int* info = reinterpret_cast<int*>(base + L.info);
-  const OrderArgs a{last, d_zero_off_, ord_cand_n_, direction, reinterpret_cast<int*>(base + L.cnt), info};
+  const OrderArgs a{reinterpret_cast<int*>(base + L.last), m_ord_, d_zero_off_, ord_cand_n_, direction,
+                    reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.info),
+                    reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
   const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
   int adv_dir = 0;
   if (rblock == 1) {
-    // last_indexes change between iterations only: uploaded at the first
-    // radius, where the previous iteration's max_block_error update runs too
+    // last_indexes change between iterations only: the first radius copies
+    // them to the device and applies the previous iteration's
+    // max_block_error update (the previous build's kernels, which read the
+    // staging, have completed: the host synchronised on them)
     memcpy(h_ord_, last_indexes.data(), static_cast<size_t>(nb_) * 4);
-    GZ_HIP(hipMemcpyAsync(last, h_ord_, static_cast<size_t>(nb_) * 4, hipMemcpyHostToDevice, s));
     adv_dir = ord_adv_dir_;
     ord_adv_dir_ = 0;
   }
   GZ_TIMED("order_build", k_order_local<<<groups, 256, 0, s>>>(d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock,
                                                                 target_distance, weight, active,
                                                                 reinterpret_cast<float*>(base + L.mbe),
-                                                                ord_adv_vt_, adv_dir, a));
+                                                                ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, a));
   if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
-  GZ_HIP(hipMemcpyAsync(h_ord_ + nb_, info, 32, hipMemcpyDeviceToHost, s));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
   *blocks_to_change = h_ord_[nb_ + rblock - 1];
@@ -1263,32 +1269,29 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!n) return true;
+  // (at most cand_n + nb: a block past the last candidate reads one, the
+  // host's clamp of its offset into [0, cand_n - 1])
+  if (n > static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_)) return Fail("OrderFetch entry count", 0);
   const size_t bytes = n * sizeof(OrderEntry);
-  if (bytes > ord_entries_cap_) {
-    if (d_ord_entries_) GZ_HIP(hipFree(d_ord_entries_));
-    d_ord_entries_ = nullptr;
-    const size_t cap = bytes + bytes / 4 + 4096;
-    GZ_HIP(hipMalloc(&d_ord_entries_, cap));
-    ord_entries_cap_ = cap;
-  }
   if (bytes > h_ord_entries_cap_) {
     if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
     h_ord_entries_ = nullptr;
     const size_t cap = bytes + bytes / 4 + 4096;
-    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap));
+    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap, hipHostMallocCoherent));
+    GZ_HIP(hipHostGetDevicePointer(&m_ord_entries_, h_ord_entries_, 0));
     h_ord_entries_cap_ = cap;
   }
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
   int* cnt = reinterpret_cast<int*>(base + L.cnt);
   int* off = reinterpret_cast<int*>(base + L.off);
-  const OrderArgs a{reinterpret_cast<const int*>(base + L.last), d_zero_off_, ord_cand_n_, ord_direction_, cnt,
-                    reinterpret_cast<int*>(base + L.info)};
+  const OrderArgs a{reinterpret_cast<int*>(base + L.last), m_ord_, d_zero_off_, ord_cand_n_, ord_direction_, cnt,
+                    reinterpret_cast<int*>(base + L.info), reinterpret_cast<uint32_t*>(base + L.arr),
+                    m_ord_ + nb_};
   if (!ScanCounts(cnt, nb_, off, "order_scan")) return false;
-  GZ_TIMED("order_fill", k_order_fill<<<(nb_ + 255) / 256, 256, 0, s>>>(
+  GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(
       reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
-      off, static_cast<OrderEntry*>(d_ord_entries_), a));
-  GZ_HIP(hipMemcpyAsync(h_ord_entries_, d_ord_entries_, bytes, hipMemcpyDeviceToHost, s));
+      off, static_cast<int>(n), static_cast<OrderEntry*>(m_ord_entries_), a));
   GZ_HIP(hipStreamSynchronize(s));
   ProfFlush();
   memcpy(static_cast<void*>(out), h_ord_entries_, bytes);

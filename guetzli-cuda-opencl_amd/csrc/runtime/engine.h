@@ -308,18 +308,17 @@ class Engine {
   // pinned host staging
   float* h_block_max_ = nullptr;
   // device change order (allocated on first use): weight f32 | active i32 |
-  // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | max_block_error f32
-  // | last_indexes i32; entries; pinned staging of last_indexes + totals and
-  // of the entries
+  // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
+  // max_block_error f32 | last_indexes i32
   int ord_cand_n_ = -1;             // candidates of the last 4:4:4 zeroing search (-1: none)
   int ord_direction_ = 0;
   float ord_adv_vt_ = 0.0f;         // pending max_block_error update (OrderAdvance)
   int ord_adv_dir_ = 0;
   void* d_ord_ = nullptr;
-  void* d_ord_entries_ = nullptr;
-  size_t ord_entries_cap_ = 0;
-  int* h_ord_ = nullptr;
-  void* h_ord_entries_ = nullptr;
+  int* h_ord_ = nullptr;            // mapped pinned: last_indexes [nb] | totals [8]
+  int* m_ord_ = nullptr;            //   (its device address)
+  void* h_ord_entries_ = nullptr;   // mapped pinned: the entries
+  void* m_ord_entries_ = nullptr;
   size_t h_ord_entries_cap_ = 0;
 };
 
