@@ -53,3 +53,25 @@ def test_png_file_encode_reproduces_reference(gz, name):
     out, st = gz.process_file(data, gz.Params.for_quality(e["quality"]), return_stats=True)
     assert st.iterations == e["iters"]
     assert hashlib.sha256(out).hexdigest() == e["sha256"]
+
+
+def _png_chunk(kind, data):
+    import struct
+    import zlib
+    return struct.pack(">I", len(data)) + kind + data + struct.pack(">I", zlib.crc32(kind + data) & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("w,h,depth,ctype", [(1000000, 1000000, 16, 6), (60000, 60000, 8, 2)])
+def test_png_decode_rejects_huge_header_with_tiny_data(gz, w, h, depth, ctype):
+    """A header promising far more pixels than its compressed data can hold
+    (deflate expands at most 1032:1) fails before anything of that size is
+    allocated -- the 'not enough image data' outcome libpng gives the
+    reference's ReadPNG -- instead of an allocation of ~8e12 bytes or an
+    exception crossing the C ABI."""
+    import struct
+    import zlib
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    data = (b"\x89PNG\r\n\x1a\n" + _png_chunk(b"IHDR", ihdr) +
+            _png_chunk(b"IDAT", zlib.compress(b"\x00" * 64)) + _png_chunk(b"IEND", b""))
+    with pytest.raises(gz.GuetzliError):
+        gz.png_decode(data)
