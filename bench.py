@@ -23,15 +23,20 @@ and a mismatch fails the run.
 
 Also reported (one JSON line on rank 0):
   single_frame  one frame encoded alone after the timed region (latency).
-  roofline      the kernel with the most GPU time per frame (today the
-                per-block zeroing search), timed with HIP events on the
-                engine's own stream inside the library (gz_profile_*) during
-                that isolated frame, against its algorithmic bytes per
-                launch; with its VALU issue utilisation from the committed
-                SQ counters (it is latency/VALU-bound, not HBM-bound).
+  roofline      north_star's: the Butteraugli blur+mask pass at 4K against
+                HBM -- one BASELINE configs[2] frame (3840x2160 q90, seed 0,
+                bytes checked) encoded alone after the timed region, the
+                pass's kernels timed with HIP events on the engine's own
+                stream inside the library (gz_profile_*), SURVEY 8(d)'s
+                272 algorithmic B/px over their summed time ("configs2_4k",
+                "blur_mask_pass_4k").
+  zeroing_roofline  the kernel with the most GPU time per frame (the
+                per-block zeroing search) in the isolated 1080p frame: VALU /
+                latency-bound, so `frac` is its vector issue utilisation from
+                the committed SQ counters; its HBM fraction is `hbm_frac`.
   compare_roofline  the same for the dominant kernel of the Butteraugli
                 Compare pass (block_diff), and blur_mask_pass for the
-                BASELINE blur+mask pass.
+                blur+mask pass of the 1080p frame.
   cpu_baseline  the reference `guetzli --c` (oracle/_ref, built from the
                 reference sources) on the host cores: one 1080p q95 frame per
                 process, 8 concurrent processes (the bench workload's frames,
@@ -455,6 +460,145 @@ def dist_selftest(args):
     return 0 if got == expect else 1
 
 
+def frame_report(prof, w, h, kept):
+    """Per-launch HIP-event report of one isolated frame (gz_profile_*):
+    stages, the Compare pass, the blur+mask pass and the kernel rooflines.
+    kept: the frame's kept zeroing entries."""
+    bpp = stage_bytes_per_px()
+    stages = {}
+    regions = []
+    for name, (cnt, ms) in prof.items():
+        if not cnt:
+            continue
+        avg = ms / cnt
+        b = region_bytes(name, w, h, kept)
+        row = {"launches": cnt, "avg_ms": round(avg, 4), "frame_ms": round(ms, 4)}
+        if b is not None:
+            row["algo_GBps"] = round(b / (avg * 1e-3) / 1e9, 1)
+        if name in bpp or name in ("block_zeroing", "jpeg_stage", "jpeg_code"):
+            stages[name] = row
+        if name != "compare_pass":
+            regions.append((ms, name, cnt))
+    regions.sort(reverse=True)
+
+    def roof_of(name):
+        cnt, ms = prof[name]
+        avg = ms / cnt
+        b = region_bytes(name, w, h, kept)
+        achieved = b / (avg * 1e-3) / 1e9
+        traffic, tsrc = measured_traffic(name, w, h)
+        r = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+             "traffic": traffic, "traffic_source": tsrc, "algo_bytes_per_launch": int(b),
+             "avg_launch_ms": round(avg, 4), "launches_per_frame": cnt,
+             "frame_gpu_ms": round(ms, 4)}
+        vi = valu_issue(name, w, h, avg)
+        if vi:
+            r["valu_issue"] = vi
+        return r
+
+    # the kernel with the most GPU time in the frame (the per-block zeroing
+    # search): VALU/latency-bound, so its ceiling is the vector issue rate
+    # (valu_issue.frac); its HBM fraction is kept beside it as hbm_frac
+    dominant = next((n for _, n, _ in regions if region_bytes(n, w, h) is not None), None)
+    dom = roof_of(dominant) if dominant else None
+    if dom is not None:
+        dom["gpu_time_share_of_frame"] = round(prof[dominant][1] / sum(ms for ms, _, _ in regions), 4)
+        if "valu_issue" in dom:
+            dom["hbm_frac"] = dom["frac"]
+            dom.update({"bound": "valu", "unit": "VALU issue fraction",
+                        "achieved": dom["valu_issue"]["frac"], "peak": 1.0,
+                        "frac": dom["valu_issue"]["frac"]})
+    # the dominant kernel of the Butteraugli Compare pass
+    cmp_rows = sorted(((prof[n][1], n) for n in bpp if n in prof and prof[n][0]), reverse=True)
+    compare_roof = roof_of(cmp_rows[0][1]) if cmp_rows else None
+    bm_ms = sum(stages[k]["avg_ms"] for k in BLUR_MASK_STAGES if k in stages)
+    blur_mask = None
+    if bm_ms > 0:
+        bm_bytes = BLUR_MASK_BYTES_PER_PX * w * h
+        blur_mask = {"algo_bytes": int(bm_bytes), "ms": round(bm_ms, 4),
+                     "achieved_GBps": round(bm_bytes / (bm_ms * 1e-3) / 1e9, 1),
+                     "frac": round(bm_bytes / (bm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "stages": [k for k in BLUR_MASK_STAGES if k in stages],
+                     "stage_ms": {k: stages[k]["avg_ms"] for k in BLUR_MASK_STAGES if k in stages}}
+        # measured HBM bytes of the same launches (committed PMC summary of
+        # this frame size), where every stage has one
+        tr = [measured_traffic(k, w, h)[0] for k in blur_mask["stages"]]
+        if tr and all(t is not None for t in tr):
+            blur_mask["traffic"] = int(sum(tr))
+            blur_mask["traffic_GBps"] = round(sum(tr) / (bm_ms * 1e-3) / 1e9, 1)
+    cp = prof.get("compare_pass")
+    pass_bytes = sum(bpp[k] for k in PASS_KERNELS) * w * h
+    compare_pass = None
+    if cp and cp[0]:
+        avg = cp[1] / cp[0]
+        compare_pass = {"launches": cp[0], "avg_ms": round(avg, 4),
+                        "algo_bytes": int(pass_bytes),
+                        "algo_GBps": round(pass_bytes / (avg * 1e-3) / 1e9, 1)}
+    return {"stages": stages, "regions": regions, "dominant": dom, "compare_roofline": compare_roof,
+            "blur_mask_pass": blur_mask, "compare_pass": compare_pass}
+
+
+def frame_config(w, h, q):
+    """Which BASELINE config a bench frame is."""
+    if (w, h) == (1920, 1080):
+        return "each frame = BASELINE configs[1] (there at q=95)%s; 8 per GPU = configs[3]'s " \
+               "per-GPU share" % ("" if q == 95 else ", here at q=%d" % q)
+    if (w, h) == (3840, 2160):
+        return "each frame = BASELINE configs[2] (there at q=90)%s" % ("" if q == 90 else ", here at q=%d" % q)
+    if (w, h) == (8192, 8192):
+        return "each frame = BASELINE configs[4] (there at q=84)"
+    return "not a BASELINE frame size"
+
+
+def uhd_frame(gz, dev):
+    """BASELINE configs[2] after the timed region: one synthetic 3840x2160
+    frame at q=90 (seed 0, whose reference bytes are committed), resident in
+    HBM, encoded alone with per-launch HIP-event timing -- north_star's
+    roofline is the Butteraugli blur+mask pass at 4K.  Bytes checked."""
+    import hashlib
+    import torch
+    w, h, q = 3840, 2160, 90
+    kn = known_answers(w, h, q).get(0)
+    t = torch.from_numpy(gz.synthetic_frame(0, w, h).reshape(-1)).to("cuda:%d" % dev)
+    torch.cuda.synchronize()
+    params = gz.Params.for_quality(q)
+    gz.profile_reset()
+    gz.profile_enable(True)
+    t0 = time.perf_counter()
+    data, st = gz.process_device(t.data_ptr(), w, h, params, device=dev, return_stats=True)
+    sec = time.perf_counter() - t0
+    gz.profile_enable(False)
+    prof = gz.profile_read()
+    detail = gz.last_process_detail()
+    rep = frame_report(prof, w, h, int(detail.get("candidates", 0)))
+    sha = hashlib.sha256(data).hexdigest()
+    return {"config": "BASELINE configs[2]: synthetic 3840x2160 q90 (seed 0), one frame alone",
+            "seconds": round(sec, 4), "iterations": st.iterations,
+            "bit_exact": bool(kn and (kn[0], kn[1]) == (sha, st.iterations)),
+            "against": "reference guetzli --c sha256 + iterations (tests/golden/manifest.json)",
+            "blur_mask_pass": rep["blur_mask_pass"], "compare_pass": rep["compare_pass"],
+            "compare_roofline": rep["compare_roofline"], "zeroing_roofline": rep["dominant"],
+            "stages": rep["stages"]}
+
+
+def north_star_roofline(uhd):
+    """The line's `roofline` (north_star): the Butteraugli blur+mask pass at
+    4K against HBM -- SURVEY 8(d)'s 272 algorithmic B/px over the summed
+    HIP-event time of the kernels carrying those stages; traffic from the
+    committed 4K PMC summary of the same kernels."""
+    bm = uhd and uhd.get("blur_mask_pass")
+    if not bm:
+        return None
+    return {"bound": "hbm", "kernel": "blur+mask pass (%s)" % ", ".join(bm["stages"]),
+            "achieved": bm["achieved_GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": bm["frac"], "traffic": bm.get("traffic"),
+            "algo_bytes_per_launch": bm["algo_bytes"], "avg_launch_ms": bm["ms"],
+            "stage_ms": bm["stage_ms"],
+            "workload": "BASELINE configs[2] frame (3840x2160 q90), %s" % (
+                "bytes verified" if uhd["bit_exact"] else "BYTES NOT VERIFIED")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -480,6 +624,9 @@ def main():
     ap.add_argument("--no-large-frame", action="store_true",
                     help="skip the BASELINE configs[4] leg (8192x8192 q84: one engine at N < 4, "
                          "4 row strips over GPUs 0-3 at N >= 4)")
+    ap.add_argument("--no-uhd-frame", action="store_true",
+                    help="skip the BASELINE configs[2] leg (one 3840x2160 q90 frame encoded alone "
+                         "after the timed region: the north_star blur+mask roofline at 4K)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU check of the multi-rank path (launcher, gloo, byte gather, "
                          "max-over-ranks timing) with stand-in payloads; no GPU")
@@ -613,71 +760,9 @@ def main():
     total_px = world * args.steps * args.frames_per_step * w * h
     value = total_px / elapsed / 1e6
 
-    bpp = stage_bytes_per_px()
-    kept = int(host.get("candidates", 0))  # the single frame's kept zeroing entries
-    stages = {}
-    regions = []
-    for name, (cnt, ms) in prof.items():
-        if not cnt:
-            continue
-        avg = ms / cnt
-        b = region_bytes(name, w, h, kept)
-        row = {"launches": cnt, "avg_ms": round(avg, 4), "frame_ms": round(ms, 4)}
-        if b is not None:
-            row["algo_GBps"] = round(b / (avg * 1e-3) / 1e9, 1)
-        if name in bpp or name in ("block_zeroing", "jpeg_stage", "jpeg_code"):
-            stages[name] = row
-        if name != "compare_pass":
-            regions.append((ms, name, cnt))
-    regions.sort(reverse=True)
-
-    def roof_of(name):
-        cnt, ms = prof[name]
-        avg = ms / cnt
-        b = region_bytes(name, w, h, kept)
-        achieved = b / (avg * 1e-3) / 1e9
-        traffic, tsrc = measured_traffic(name, w, h)
-        r = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
-             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-             "traffic": traffic, "traffic_source": tsrc, "algo_bytes_per_launch": int(b),
-             "avg_launch_ms": round(avg, 4), "launches_per_frame": cnt,
-             "frame_gpu_ms": round(ms, 4)}
-        vi = valu_issue(name, w, h, avg)
-        if vi:
-            r["valu_issue"] = vi
-        return r
-
-    # the roofline line: the kernel with the most GPU time in the frame
-    dominant = next((n for _, n, _ in regions if region_bytes(n, w, h) is not None), None)
-    roof = roof_of(dominant) if dominant else None
-    if roof is not None:
-        roof["gpu_time_share_of_frame"] = round(
-            prof[dominant][1] / sum(ms for ms, _, _ in regions), 4)
-    # the dominant kernel of the Butteraugli Compare pass
-    cmp_rows = sorted(((prof[n][1], n) for n in bpp if n in prof and prof[n][0]), reverse=True)
-    compare_roof = roof_of(cmp_rows[0][1]) if cmp_rows else None
-    bm_ms = sum(stages[k]["avg_ms"] for k in BLUR_MASK_STAGES if k in stages)
-    blur_mask = None
-    if bm_ms > 0:
-        bm_bytes = BLUR_MASK_BYTES_PER_PX * w * h
-        blur_mask = {"algo_bytes": int(bm_bytes), "ms": round(bm_ms, 4),
-                     "achieved_GBps": round(bm_bytes / (bm_ms * 1e-3) / 1e9, 1),
-                     "frac": round(bm_bytes / (bm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "stages": [k for k in BLUR_MASK_STAGES if k in stages]}
-        # measured HBM bytes of the same launches (committed PMC summary of
-        # this frame size), where every stage has one
-        tr = [measured_traffic(k, w, h)[0] for k in blur_mask["stages"]]
-        if tr and all(t is not None for t in tr):
-            blur_mask["traffic"] = int(sum(tr))
-            blur_mask["traffic_GBps"] = round(sum(tr) / (bm_ms * 1e-3) / 1e9, 1)
-    cp = prof.get("compare_pass")
-    pass_bytes = sum(bpp[k] for k in PASS_KERNELS) * w * h
-    compare_pass = None
-    if cp and cp[0]:
-        avg = cp[1] / cp[0]
-        compare_pass = {"launches": cp[0], "avg_ms": round(avg, 4),
-                        "algo_bytes": int(pass_bytes),
-                        "algo_GBps": round(pass_bytes / (avg * 1e-3) / 1e9, 1)}
+    rep = frame_report(prof, w, h, int(host.get("candidates", 0)))
+    regions = rep["regions"]
+    uhd = None if args.no_uhd_frame else uhd_frame(gz, dev)
     gpu_frame_ms = sum(ms for ms, _, _ in regions)
 
     out = {
@@ -694,9 +779,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": "%d synthetic %dx%d sRGB frames per GPU per step, %d encoding "
-                               "at once, q=%d, guetzli::Process end to end (each frame = BASELINE "
-                               "configs[1]; 8 per GPU = configs[3]'s per-GPU share)" % (
-                                   args.frames_per_step, w, h, in_flight, q),
+                               "at once, q=%d, guetzli::Process end to end (%s)" % (
+                                   args.frames_per_step, w, h, in_flight, q, frame_config(w, h, q)),
                    "width": w, "height": h, "quality": q,
                    "frames_per_gpu_per_step": args.frames_per_step,
                    "frames_in_flight": in_flight,
@@ -709,11 +793,12 @@ def main():
         "verified": {"frames": counts[0], "bit_exact": counts[1],
                      "against": "reference guetzli --c sha256 + iterations "
                                 "(tests/golden/manifest.json)"},
-        "roofline": roof,
-        "compare_roofline": compare_roof,
-        "compare_pass": compare_pass,
-        "blur_mask_pass": blur_mask,
-        "stages": stages,
+        "roofline": north_star_roofline(uhd) or rep["dominant"],
+        "zeroing_roofline": rep["dominant"],
+        "compare_roofline": rep["compare_roofline"],
+        "compare_pass": rep["compare_pass"],
+        "blur_mask_pass": rep["blur_mask_pass"],
+        "stages": rep["stages"],
         "gpu_ms_per_frame_isolated": round(gpu_frame_ms, 3),
         "gpu_regions_ms_per_frame": {n: round(ms, 4) for ms, n, _ in regions},
         "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
@@ -727,6 +812,9 @@ def main():
                          "iterations": st1.iterations,
                          "host_breakdown_seconds": {k: round(v, 4) for k, v in host.items()}},
     }
+    if uhd is not None:
+        out["configs2_4k"] = uhd
+        out["blur_mask_pass_4k"] = uhd["blur_mask_pass"]
     if large is not None:
         out["configs4_8192"] = large
     if not args.no_cpu_baseline and world == 1:

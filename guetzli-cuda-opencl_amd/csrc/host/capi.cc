@@ -36,8 +36,35 @@ gz_status SetError(gz_status st, const std::string& msg) {
 // No C++ exception may cross the C ABI (it would terminate the caller's
 // process): host allocation failure becomes GZ_ERR_OUT_OF_MEMORY, anything
 // else GZ_ERR_INTERNAL.
+#ifndef GZ_HOSTARCH
+#define GZ_HOSTARCH ""
+#endif
+
+// The host objects are built for HOSTARCH (Makefile; x86-64-v3 by default:
+// AVX2, FMA, BMI2).  This file is not, so every entry point can check the
+// CPU before any of that code runs.
+bool HostCpuOk() {
+  static const bool ok = [] {
+    if (std::strstr(GZ_HOSTARCH, "x86-64-v3") == nullptr) return true;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") &&
+           __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("f16c") &&
+           __builtin_cpu_supports("movbe");
+  }();
+  return ok;
+}
+
+gz_status CpuError(const char* what) {
+  return SetError(GZ_ERR_UNSUPPORTED, std::string(what) +
+                                          ": this libguetzli_hip was built for x86-64-v3 (AVX2, FMA, BMI2) "
+                                          "and the CPU lacks it; rebuild with `make HOSTARCH=`");
+}
+#define GZ_CPU_CHECK(what) \
+  if (!HostCpuOk()) return CpuError(what)
+
 template <class F>
 gz_status Guard(const char* what, F&& body) {
+  GZ_CPU_CHECK(what);
   try {
     return body();
   } catch (const std::bad_alloc&) {
@@ -346,6 +373,7 @@ size_t gz_profile_names(char* buf, size_t cap) {
 }
 
 gz_status gz_synthetic_frame(uint64_t seed, int width, int height, uint8_t* rgb_out) {
+  GZ_CPU_CHECK("synthetic_frame");
   if (!rgb_out || width <= 0 || height <= 0)
     return SetError(GZ_ERR_INVALID_ARG, "synthetic_frame: bad argument");
   gz::SyntheticFrame(seed, width, height, rgb_out);
@@ -353,6 +381,7 @@ gz_status gz_synthetic_frame(uint64_t seed, int width, int height, uint8_t* rgb_
 }
 
 gz_status gz_rgb_to_coeffs(const uint8_t* rgb, int width, int height, int16_t* coeffs_out) {
+  GZ_CPU_CHECK("rgb_to_coeffs");
   if (!rgb || !coeffs_out || width <= 0 || height <= 0 || width >= (1 << 16) ||
       height >= (1 << 16))
     return SetError(GZ_ERR_INVALID_ARG, "rgb_to_coeffs: bad argument");
@@ -368,6 +397,7 @@ gz_status gz_block_error_adjustment_weights(int width, int height, float target,
                                             int max_block_dist, double target_mul, int factor_x,
                                             int factor_y, const float* distmap,
                                             float* block_weight) {
+  GZ_CPU_CHECK("block_error_adjustment_weights");
   if (!distmap || !block_weight || width <= 0 || height <= 0 || factor_x < 1 || factor_y < 1 ||
       (direction != 1 && direction != -1) || max_block_dist < 0)
     return SetError(GZ_ERR_INVALID_ARG, "block_error_adjustment_weights: bad argument");
@@ -553,6 +583,7 @@ gz_status gz_process_rgb_strips(int device, const gz_params* params, const uint8
 
 gz_status gz_strip_layout(int width, int height, int world, int rank, int* y0, int* y1, int* e0,
                           int* e1) {
+  GZ_CPU_CHECK("strip_layout");
   if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || !y0 || !y1 || !e0 ||
       !e1)
     return SetError(GZ_ERR_INVALID_ARG, "strip_layout: bad argument");
@@ -565,6 +596,7 @@ gz_status gz_strip_layout(int width, int height, int world, int rank, int* y0, i
 }
 
 gz_status gz_collectives_selftest(const gz_collectives* coll) {
+  GZ_CPU_CHECK("collectives_selftest");
   if (!ValidCollectives(coll)) return SetError(GZ_ERR_INVALID_ARG, "collectives: bad argument");
   CCollectives cc(coll);
   // equal-size gather of a rank-tagged pattern, then a variable-size one

@@ -23,6 +23,7 @@
 #pragma once
 
 #include <stddef.h>
+#include <stdint.h>
 
 #include <algorithm>
 #include <utility>
@@ -119,7 +120,8 @@ class LazyStdSort {
   size_t Cut(Elem* f, Elem* l) {
     Elem* mid = f + (l - f) / 2;
     MoveMedianToFirst(f, f + 1, mid, l - 1);
-    Elem* c = static_cast<size_t>(l - f) >= kParallelMin ? ParallelPartition(f, l)
+    const size_t len = static_cast<size_t>(l - f);
+    Elem* c = len >= kParallelMin && len <= 0xffffffffu ? ParallelPartition(f, l)
                                                           : UnguardedPartition(f + 1, l, f);
     return static_cast<size_t>(c - a_);
   }
@@ -130,7 +132,8 @@ class LazyStdSort {
   // sequential loop swaps exactly these pairs (no scan meets a swapped
   // position before the pointers cross); with K the first k where L[k] >=
   // R[k], its last left scan stops at min(L[K], R[K - 1]) -- R[K - 1] now
-  // holds an element not below the pivot -- which is the cut.
+  // holds an element not below the pivot -- which is the cut.  Positions are
+  // u32 (the range is under 2^32): 4 B per entry of L and R at a cut.
   Elem* ParallelPartition(Elem* f, Elem* l) {
     const float pv = f->second;
     const size_t n = static_cast<size_t>(l - f);
@@ -152,13 +155,13 @@ class LazyStdSort {
       nr[c + 1] += nr[c];
     }
     const size_t cl = nl[chunks], cr = nr[chunks];
-    std::vector<size_t> L(cl), R(cr);
+    std::vector<uint32_t> L(cl), R(cr);
     ParallelFor(chunks, [&](int c) {
       size_t a = nl[c], b = cr - nr[c];  // R descending: chunk c's last slot
       for (size_t i = c * per; i < std::min(n, (c + 1) * per); ++i) {
         const float k = f[i].second;
-        if (i > 0 && !(k < pv)) L[a++] = i;
-        if (!(pv < k)) R[--b] = i;
+        if (i > 0 && !(k < pv)) L[a++] = static_cast<uint32_t>(i);
+        if (!(pv < k)) R[--b] = static_cast<uint32_t>(i);
       }
     });
     // K: first k with L[k] >= R[k] (L rises, R falls)
@@ -175,8 +178,8 @@ class LazyStdSort {
         for (size_t k = c * sp; k < std::min(K, (c + 1) * sp); ++k) std::swap(f[L[k]], f[R[k]]);
       });
     }
-    size_t cut = K < cl ? L[K] : n;
-    if (K > 0) cut = std::min(cut, R[K - 1]);
+    size_t cut = K < cl ? static_cast<size_t>(L[K]) : n;
+    if (K > 0) cut = std::min(cut, static_cast<size_t>(R[K - 1]));
     return f + cut;
   }
 

@@ -565,12 +565,14 @@ bool HipButteraugliComparator::BlockZeroingCandidates420(Image420* img, int comp
   return true;
 }
 
-bool HipButteraugliComparator::DeviceOrderReset() {
-  if (!engine_->HasOrderCandidates()) return false;
+bool HipButteraugliComparator::DeviceOrderReset(bool* available) {
+  *available = false;
+  if (!engine_->HasOrderCandidates()) return true;
   if (!engine_->OrderReset()) {
     err_ = engine_->error();
     return false;
   }
+  *available = true;
   return true;
 }
 
@@ -1288,7 +1290,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // the change order on the device (weights, entries, max_block_error there;
   // the frame's candidates and block maxima are resident) unless the frame
   // is split over ranks or the comparator has no device
-  const bool device_order = !part_ && cmp_->DeviceOrderReset();
+  bool device_order = false;
+  if (!part_ && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early) FlushOutput();  // best_size_ must be current

@@ -105,8 +105,12 @@ class Comparator {
   // 0), DeviceChangeOrder per iteration (the weights at radius 1..4 until
   // some block has entries; the entries in block order, as
   // Processor::BuildChangeOrder makes them), DeviceOrderAdvance after it.
-  // False from DeviceOrderReset: not available, build on the host.
-  virtual bool DeviceOrderReset() { return false; }
+  // DeviceOrderReset: false on an engine error (error() says which);
+  // *available = false: no device order, build on the host.
+  virtual bool DeviceOrderReset(bool* available) {
+    *available = false;
+    return true;
+  }
   virtual bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax,
                                  const std::vector<int>& last_indexes,
                                  std::vector<std::pair<int, float>>* order, int* blocks_to_change) {
@@ -211,7 +215,7 @@ class HipButteraugliComparator : public Comparator {
                                           const std::vector<float>& max_dist_per_block,
                                           std::vector<float>* block_weight) override;
   const std::string& error() const override { return err_; }
-  bool DeviceOrderReset() override;
+  bool DeviceOrderReset(bool* available) override;
   bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
                          std::vector<std::pair<int, float>>* order, int* blocks_to_change) override;
   bool DeviceOrderAdvance(float val_threshold, int direction) override;

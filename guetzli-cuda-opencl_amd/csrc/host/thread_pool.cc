@@ -157,16 +157,15 @@ Pool* GetPool() {
 namespace {
 // CPUs this process may use: its affinity set (sched_getaffinity), capped by
 // a cgroup v2 CPU quota (cpu.max "quota period"; a container's CPU share is
-// often a quota, not an affinity mask).  *pinned: the affinity set is smaller
-// than the online CPUs, i.e. someone (taskset, numactl, a launcher) already
-// gave this process its share.
-int UsableCpus(bool* pinned) {
-  const int online = std::max(1, static_cast<int>(std::thread::hardware_concurrency()));
-  int n = online;
+// often a quota, not an affinity mask).  *affinity: the affinity set's size,
+// *online: the online CPUs.
+int UsableCpus(int* affinity, int* online) {
+  *online = std::max(1, static_cast<int>(std::thread::hardware_concurrency()));
+  int n = *online;
   cpu_set_t set;
   CPU_ZERO(&set);
   if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = CPU_COUNT(&set);
-  *pinned = n < online;
+  *affinity = n;
   if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
     char quota[32] = {0};
     long period = 0;
@@ -187,13 +186,17 @@ int HostThreads() {
   static const int n = [] {
     const char* e = std::getenv("GZ_HOST_THREADS");
     if (e && std::atoi(e) > 0) return std::min(256, std::atoi(e));
-    // the node's CPUs shared by the ranks on it (torch.distributed.run sets
-    // LOCAL_WORLD_SIZE) unless this rank is pinned to its own cpuset, at
-    // most 16 per process
-    bool pinned = false;
-    int share = UsableCpus(&pinned);
+    // the usable CPUs shared by the ranks on the node (torch.distributed.run
+    // sets LOCAL_WORLD_SIZE), at most 16 per process -- unless this rank's
+    // affinity set is already no larger than its share of the online CPUs
+    // (a launcher pinned each rank to its own cpuset).  A container's cpuset
+    // smaller than the host is not a per-rank pinning: the ranks share it.
+    int affinity = 0, online = 0;
+    int share = UsableCpus(&affinity, &online);
     const char* lw = std::getenv("LOCAL_WORLD_SIZE");
-    if (!pinned && lw && std::atoi(lw) > 1) share /= std::atoi(lw);
+    const int local = lw ? std::max(1, std::atoi(lw)) : 1;
+    const bool pinned = local > 1 && affinity <= online / local;
+    if (!pinned && local > 1) share /= local;
     return std::max(1, std::min(16, share));
   }();
   return n;

@@ -454,9 +454,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_jwords_[1]), e->jwords_cap_ * 4);
   const size_t code_groups = (static_cast<size_t>(e->nb_) + kCodeMcus - 1) / kCodeMcus;
-  // 0xff counters | arrival counters | status words | shared words
+  // 0xff counters | arrival counters | status words | shared words | seam counters
   const size_t jctl_bytes = kCodeFfCopies * 8 + (1 + code_groups / 64 + 2) * 8 + code_groups * 8 +
-                            code_groups * 16;
+                            code_groups * 16 + (code_groups + 1) * 4;
   alloc(reinterpret_cast<void**>(&e->d_jctl_), jctl_bytes);
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 64, hipHostMallocCoherent) != hipSuccess)
     ok = false;
@@ -1214,12 +1214,25 @@ bool Engine::OrderReset() {
   GZ_HIP(hipSetDevice(device_));
   const OrdLayout L(nb_);
   if (!d_ord_) {
-    GZ_HIP(hipMalloc(&d_ord_, L.bytes));
+    // (all three buffers or none: they are committed together)
+    void* d = nullptr;
+    int* h = nullptr;
+    int* m = nullptr;
+    const bool ok =
+        hipMalloc(&d, L.bytes) == hipSuccess &&
+        hipHostMalloc(reinterpret_cast<void**>(&h), static_cast<size_t>(nb_) * 4 + 64, hipHostMallocCoherent) ==
+            hipSuccess &&
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&m), h, 0) == hipSuccess &&
+        hipMemsetAsync(static_cast<char*>(d) + L.info, 0, L.mbe - L.info, s) == hipSuccess;  // totals, arrivals
+    if (!ok) {
+      if (d) (void)hipFree(d);
+      if (h) (void)hipHostFree(h);
+      return Fail("OrderReset: device allocation failed", 0);
+    }
+    d_ord_ = d;
+    h_ord_ = h;
+    m_ord_ = m;
     bytes_ += L.bytes;
-    GZ_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ord_), static_cast<size_t>(nb_) * 4 + 64,
-                         hipHostMallocCoherent));
-    GZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_ord_), h_ord_, 0));
-    GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.info, 0, L.mbe - L.info, s));  // totals, arrivals
   }
   GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
   ord_adv_dir_ = 0;
@@ -1437,18 +1450,18 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0
   // scan of these MCUs, plus the word of an unaligned start)
   uint32_t* words = d_jwords_[jslot_];
   const int groups = (m1 - m0 + kCodeMcus - 1) / kCodeMcus;
-  // launch counter: tags the status words (low 14 bits) and the published
-  // shared words (all 32; 0 is the zeroed arrays' tag, never used)
-  if (++jepoch_ == 0) jepoch_ = 1;
+  // launch counter: tags the status words (low 14 bits)
+  if ((++jepoch_ & 0x3fff) == 0) ++jepoch_;  // (0: the zeroed words' tag)
   const size_t max_groups = (static_cast<size_t>(nb_) + kCodeMcus - 1) / kCodeMcus;
   unsigned long long* ffc = reinterpret_cast<unsigned long long*>(d_jctl_);
   uint32_t* arr = d_jctl_ + 2 * kCodeFfCopies;
   uint64_t* status = reinterpret_cast<uint64_t*>(arr) + 1 + max_groups / 64 + 2;
   uint64_t* side = status + max_groups;
+  uint32_t* seam = reinterpret_cast<uint32_t*>(side + 2 * max_groups);
   GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_jzz_, nb_, m0, m1, ncomp, dc,
                                                             static_cast<unsigned long long>(base),
                                                             pad_end ? 1 : 0, words, ffc, arr, status, side,
-                                                            jepoch_, m_jhist_ + 6 * 256 + 2));
+                                                            seam, jepoch_, m_jhist_ + 6 * 256 + 2));
   jpart_[jslot_].base = base;
   // (0xff count, bit total, shared words) reach h_jhist_[1538..1543] from
   // the last workgroup to finish

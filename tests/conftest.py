@@ -23,6 +23,21 @@ def _ensure_built():
     if not os.path.exists(oracle):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], check=True,
                        stdout=subprocess.DEVNULL)
+    occupy = os.path.join(ROOT, "tests", "_build", "libgz_occupy.so")
+    src = os.path.join(ROOT, "tests", "native", "occupy.hip")
+    if not os.path.exists(occupy) or os.path.getmtime(occupy) < os.path.getmtime(src):
+        build_occupy()
+
+
+def build_occupy():
+    """tests/native/occupy.hip -> tests/_build/libgz_occupy.so (a GPU test's
+    slot-holding kernel; built here on the CPU, it travels with the tree)."""
+    out = os.path.join(ROOT, "tests", "_build", "libgz_occupy.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = "%s.%d.tmp" % (out, os.getpid())
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-shared", "-fPIC", "--offload-arch=gfx950",
+                    os.path.join(ROOT, "tests", "native", "occupy.hip"), "-o", tmp], check=True)
+    os.replace(tmp, out)
 
 
 _ensure_built()

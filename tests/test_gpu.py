@@ -178,6 +178,58 @@ def test_device_jpeg_writer_matches_host_writer(gz, w, h, seed):
         assert dev == host, "trial %d: %d vs %d bytes" % (trial, len(dev), len(host))
 
 
+def _occupy_lib():
+    """tests/native/occupy.hip (built by __graft_entry__.build / conftest)."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build",
+                                 "libgz_occupy.so"))
+    L.occupy_start.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.occupy_start.restype = ctypes.c_void_p
+    L.occupy_held.argtypes = [ctypes.c_void_p]
+    L.occupy_release.argtypes = [ctypes.c_void_p]
+    return L
+
+
+@pytest.mark.parametrize("spare_xcd", [0, 5])
+def test_coder_forward_progress_under_occupancy(gz, spare_xcd):
+    """k_jpeg_code never waits without bound on a workgroup that has not been
+    dispatched (jpeg_kernels.inc: look-back fallback + seam counters).
+    Another stream's kernel holds every CU but those of one XCD (one
+    workgroup with all 160 KiB of LDS per CU); three engines code a 1080p
+    candidate at once while it holds, then the host releases it: every
+    coder finishes with the host writer's bytes."""
+    import concurrent.futures
+    import time
+    w, h = 1920, 1080
+    rng = np.random.default_rng(31 + spare_xcd)
+    rgb = gz.synthetic_frame(4, w, h)
+    quant = rng.integers(1, 40, size=(3, 64)).astype(np.int32)
+    co = _quantized(gz, rgb, w, h, quant).reshape(-1)
+    host = gz.write_jpeg_host(co, quant, w, h)
+    cmps = [gz.ButteraugliComparator(w, h, rgb, 1.0) for _ in range(3)]
+    for c in cmps:
+        assert c.write_jpeg(co, quant) == host  # warm (engines, code paths)
+    L = _occupy_lib()
+    occ = L.occupy_start(0, spare_xcd, 20000)
+    assert occ, "occupy_start failed"
+    released = False
+    try:
+        time.sleep(0.2)
+        held = L.occupy_held(occ)
+        with concurrent.futures.ThreadPoolExecutor(max_workers=3) as ex:
+            futs = [ex.submit(c.write_jpeg, co, quant) for c in cmps]
+            time.sleep(0.3)
+            assert L.occupy_release(occ) == 0
+            released = True
+            outs = [f.result(timeout=60) for f in futs]
+    finally:
+        if not released:
+            L.occupy_release(occ)
+    assert held >= 160, "the holding kernel held only %d CUs" % held
+    for i, o in enumerate(outs):
+        assert o == host, "engine %d: %d vs %d bytes" % (i, len(o), len(host))
+
+
 def _jpeg_sha(gz, rgb, w, h, q):
     data, stats = gz.process(rgb, w, h, gz.Params.for_quality(q), return_stats=True)
     return hashlib.sha256(data).hexdigest(), stats
