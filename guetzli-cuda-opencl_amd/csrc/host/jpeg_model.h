@@ -68,6 +68,11 @@ struct CoeffImage {
   // False while only a device mirror holds the current coefficients (after a
   // device-side global quantization whose host copy was not requested).
   bool host_valid = true;
+  // True while the search back end keeps the host copy lazily: some blocks
+  // lag changes made on the device copy alone (Processor materialises a
+  // block before it reads or journals it).  The journalled entries are
+  // current, so a mirror may replay the journal but not re-read the rest.
+  bool host_partial = false;
   void MarkChanged(int c, int block_ix, int k) {
     changed.push_back(static_cast<uint32_t>((static_cast<size_t>(c) * blocks + block_ix) * 64 + k));
   }
@@ -75,6 +80,7 @@ struct CoeffImage {
     ++epoch;
     changed.clear();
     host_valid = true;
+    host_partial = false;
   }
 
   void Init(int w, int h);

@@ -157,12 +157,13 @@ bool HipButteraugliComparator::IsOriginal(const CoeffImage& img) const {
 // journalled edits when it is in img's epoch, else everything.
 bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
   if (device_.Current(img)) return true;
-  if (!img.host_valid) {
+  const bool replay = device_.CanReplay(img) && img.changed.size() - device_.pos < img.coeffs.size() / 8;
+  if (!img.host_valid || (img.host_partial && !replay)) {
     err_ = "coefficients are current on neither side";
     return false;
   }
   bool ok;
-  if (device_.CanReplay(img) && img.changed.size() - device_.pos < img.coeffs.size() / 8) {
+  if (replay) {
     const size_t n = img.changed.size() - device_.pos;
     const uint32_t* idx = img.changed.data() + device_.pos;
     delta_val_.resize(n);
@@ -598,6 +599,22 @@ bool HipButteraugliComparator::DeviceChangeOrder(int direction, double target_mu
       break;
     }
   }
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt,
+                                               JpegHistogram ac[3]) {
+  const auto t0 = Clock::now();
+  if (!SyncCoeffs(img)) return false;
+  uint32_t hist[6 * 256];
+  uint64_t chroma = 0;
+  if (!engine_->BulkApply(direction, img.quant, cnt, hist, &chroma)) {
+    err_ = engine_->error();
+    return false;
+  }
+  JpegHistogram dc[3];
+  HistogramsFromStage(hist, chroma, dc, ac);
+  seconds_bulk += Since(t0);
   return true;
 }
 
@@ -1292,6 +1309,39 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // is split over ranks or the comparator has no device
   bool device_order = false;
   if (!part_ && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
+  // With the device order the bulk prefix is applied on the device too
+  // (DeviceBulkApply), with the AC histograms recounted there.  The host copy
+  // of a block then follows lazily: a block's coefficients are a function of
+  // its last_indexes alone -- its first last_indexes[b] candidates zeroed,
+  // the others as quantized (up iterations zero candidates in order, down
+  // iterations restore them in reverse) -- so mat_li[b], the last_indexes the
+  // host copy reflects, is brought up to date (materialize) before the tail
+  // reads or changes the block.
+  const bool device_bulk = device_order && cmp_->HasDeviceBulk();
+  std::vector<int> mat_li;
+  std::vector<uint8_t> bulk_cnt8;
+  if (device_bulk) mat_li.assign(num_blocks, 0);
+  auto materialize = [&](int bix) {
+    int m = mat_li[bix];
+    const int li = last_indexes[bix];
+    if (m == li) return;
+    const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+    const int bx = bix % block_width, by = bix / block_width;
+    for (; m != li; m += m < li ? 1 : -1) {
+      const int idx = cand[offset + (m < li ? m : m - 1)];
+      const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
+      coeff_t v = 0;
+      if (m > li) {
+        const JpegComponent& comp = jpg.components[c];
+        v = QuantizeCoeff(comp.coeffs[static_cast<size_t>(by * comp.width_in_blocks + bx) * 64 + k], img->quant[c][k]);
+      }
+      img->block(c, bix)[k] = v;
+      uint64_t& nzm = acm.nz[static_cast<size_t>(c) * num_blocks + bix];
+      const int z = kJPEGZigZagOrder[k];
+      if (v) nzm |= 1ull << z; else nzm &= ~(1ull << z);
+    }
+    mat_li[bix] = li;
+  };
   for (int direction : {1, -1}) {
     for (;;) {
       if (stop_early) FlushOutput();  // best_size_ must be current
@@ -1357,12 +1407,37 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           });
         }
+        if (device_bulk) {
+          // the changes on the device and a recount of the AC histograms
+          // there; the host only advances last_indexes (blocks materialise
+          // lazily)
+          bulk_cnt8.resize(num_blocks);
+          // (a few ns per block: on the pool only for very large frames)
+          const int slices = own_hi - own_lo >= (1 << 19) ? 16 : 1;
+          ParallelFor(slices, [&](int sl) {
+            const int b0 = own_lo + static_cast<int>(static_cast<int64_t>(own_hi - own_lo) * sl / slices);
+            const int b1 = own_lo + static_cast<int>(static_cast<int64_t>(own_hi - own_lo) * (sl + 1) / slices);
+            for (int bix = b0; bix < b1; ++bix) {
+              bulk_cnt8[bix] = static_cast<uint8_t>(bulk_cnt_[bix]);
+              last_indexes[bix] += bulk_cnt_[bix] * direction;
+            }
+          });
+          JpegHistogram ac_now[3];
+          if (!cmp_->DeviceBulkApply(*img, direction, bulk_cnt8.data(), ac_now)) return Fail(err);
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          img->host_partial = true;
+          refresh_raw();
+          loop.changed = static_cast<int>(bulk);
+          res_->detail["backend_bulk_s"] += Since(tbk);
+          res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+          res_->detail["backend_bulk_device"] += 1;
+        }
         struct ChunkDelta {
           JpegHistogram h[3];
           std::vector<uint32_t> changed;
         };
-        std::vector<ChunkDelta> deltas(own_chunks);
-        ParallelFor(own_chunks, [&](int ch) {
+        std::vector<ChunkDelta> deltas(device_bulk ? 0 : own_chunks);
+        if (!device_bulk) ParallelFor(own_chunks, [&](int ch) {
           ChunkDelta& d = deltas[ch];
           int64_t raw_unused = 0;
           const int b0 = own_lo + ch * kOrderChunk, b1 = std::min(own_hi, b0 + kOrderChunk);
@@ -1423,6 +1498,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             last_indexes[bix] = li;
           }
         });
+        if (!device_bulk) {
         // (symbols only: the last slot is the histogram's fixed sentinel count)
         std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1), 0);
         for (const ChunkDelta& d : deltas) {
@@ -1440,6 +1516,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         loop.changed = static_cast<int>(bulk);
         res_->detail["backend_bulk_s"] += Since(tbk);
         res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+        }
       }
       const size_t n_order = global_order.size();
       double codes_s = 0.0;
@@ -1463,6 +1540,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // the change of the next entry of owned block bix applied to img: its
       // symbol updates into the frame's histograms, or (log) recorded
       auto apply = [&](int bix, SymbolLog* log) {
+        if (device_bulk) materialize(bix);
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
         const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
@@ -1482,6 +1560,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
         img->MarkChanged(c, bix, k);
         last_indexes[bix] += direction;
+        if (device_bulk) mat_li[bix] = last_indexes[bix];
       };
       if (!part_ || part_->world == 1) {
         // Prefetch window: when the lazy sort hands out a new sorted chunk, the
@@ -1625,6 +1704,13 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       if (!EncodeAndCompare(jpg, *img, err)) return false;
       prev_size = est_jpg_size;
     }
+  }
+  if (device_bulk) {
+    // the device copy is the image now; nothing after the back end reads
+    // the host copy before the next bulk rewrite (CopyFromJpegData) -- a
+    // mirror that would have to read it fails instead (host_valid)
+    img->host_valid = false;
+    img->host_partial = false;
   }
   FlushOutput();
   return true;

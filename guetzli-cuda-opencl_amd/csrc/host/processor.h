@@ -117,6 +117,16 @@ class Comparator {
     return false;
   }
   virtual bool DeviceOrderAdvance(float val_threshold, int direction) { return false; }
+  // The back end's bulk prefix on the device (with the device order only):
+  // cnt[b] (< 256) changes of block b from the last_indexes of the last
+  // DeviceChangeOrder, in `direction`, applied to the device copy of img
+  // alone (the caller brings its host copy along lazily, host_partial), and
+  // the AC histograms of the changed image (as DeviceHistograms stores them)
+  // into ac.  HasDeviceBulk() false: apply it on the host.
+  virtual bool HasDeviceBulk() const { return false; }
+  virtual bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) {
+    return false;
+  }
   // Makes the q=1 coefficients of the original image available to
   // QuantizeFromOriginal / BlockZeroingOrders.
   virtual bool SetOriginalCoeffs(const JpegData& jpg) = 0;
@@ -219,6 +229,8 @@ class HipButteraugliComparator : public Comparator {
   bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
                          std::vector<std::pair<int, float>>* order, int* blocks_to_change) override;
   bool DeviceOrderAdvance(float val_threshold, int direction) override;
+  bool HasDeviceBulk() const override { return true; }
+  bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   bool SetOriginalCoeffs420(const JpegData& jpg420) override;
   bool Compare420(const Image420& img) override;
@@ -235,6 +247,7 @@ class HipButteraugliComparator : public Comparator {
   double cpu_compare = 0.0;  // calling thread's CPU seconds in the compares
   double seconds_wait = 0.0, cpu_wait = 0.0;  // of which waiting for the device (wall, CPU)
   double seconds_zeroing = 0.0;
+  double seconds_bulk = 0.0;  // DeviceBulkApply (wall)
   int compares = 0;
 
  private:

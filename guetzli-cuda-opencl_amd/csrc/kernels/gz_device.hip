@@ -617,6 +617,7 @@ Engine::~Engine() {
   if (h_coeffs_) hipHostFree(h_coeffs_);
   if (h_jhist_) hipHostFree(h_jhist_);
   if (h_jcodes_) hipHostFree(h_jcodes_);
+  if (h_bulk_) (void)hipHostFree(h_bulk_);
   if (h_jbytes_) hipHostFree(h_jbytes_);
   if (h_cand_idx_) hipHostFree(h_cand_idx_);
   if (h_cand_err_) hipHostFree(h_cand_err_);
@@ -1122,7 +1123,7 @@ bool Engine::BlockZeroingOrders(int comp_mask, float limit, int lookahead, bool 
   BzTraceDump(tr, nb_, stream_);
   GZ_HIP(hipMemcpyAsync(out, d_zero_out_, static_cast<size_t>(nb_) * 192 * sizeof(CoeffData),
                         hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitOnStream(s));
   ProfFlush();
   return true;
 }
@@ -1161,7 +1162,7 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
         static_cast<const CoeffData*>(d_zero_out_), d_zero_off_, nblocks, limit, d_cand_idx_, d_cand_err_));
   }
   GZ_HIP(hipMemcpyAsync(h_zero_off_, d_zero_off_, static_cast<size_t>(nblocks + 1) * 4, hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitOnStream(s));  // (behind the zeroing search: milliseconds, sleep through them)
   const size_t total = static_cast<size_t>(h_zero_off_[nblocks]);
   if (total > h_cand_cap_) {
     if (h_cand_idx_) GZ_HIP(hipHostFree(h_cand_idx_));
@@ -1269,7 +1270,7 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
                                                                 reinterpret_cast<float*>(base + L.mbe),
                                                                 ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, a));
   if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitOnStream(s));
   ProfFlush();
   *blocks_to_change = h_ord_[nb_ + rblock - 1];
   *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
@@ -1305,9 +1306,46 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(
       reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
       off, static_cast<int>(n), static_cast<OrderEntry*>(m_ord_entries_), a));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitOnStream(s));
   ProfFlush();
   memcpy(static_cast<void*>(out), h_ord_entries_, bytes);
+  return true;
+}
+
+bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, uint32_t* hist,
+                       uint64_t* chroma_nz) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (ord_cand_n_ < 0 || !d_ord_) return Fail("BulkApply without a change order", 0);
+  if (!h_bulk_) {
+    void* h = nullptr;
+    void* m = nullptr;
+    if (hipHostMalloc(&h, static_cast<size_t>(nb_) + 64, hipHostMallocCoherent) != hipSuccess) {
+      return Fail("BulkApply: pinned allocation failed", 0);
+    }
+    if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return Fail("BulkApply: mapped address", 0);
+    }
+    h_bulk_ = static_cast<uint8_t*>(h);
+    m_bulk_ = static_cast<uint8_t*>(m);
+    bytes_ += static_cast<size_t>(nb_) + 64;
+  }
+  // (the previous BulkApply's kernel, which read the staging, has completed:
+  // its histograms were waited for)
+  memcpy(h_bulk_, cnt, static_cast<size_t>(nb_));
+  const OrdLayout L(nb_);
+  QuantMatrix qm;
+  memcpy(qm.q, quant, sizeof(qm.q));
+  GZ_TIMED("bulk_apply", k_bulk_apply<<<static_cast<unsigned>((nb_ + 255) / 256), 256, 0, s>>>(
+      m_bulk_, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
+      d_cand_idx_, nb_, direction, d_orig_, qm, d_cur_));
+  if (!JpegStageEnqueue(quant)) return false;
+  // (a sleeping wait: nothing else of this frame is queued behind it)
+  GZ_HIP(WaitOnStream(s));
+  ProfFlush();
+  memcpy(hist, h_jhist_, 6 * 256 * 4);
+  memcpy(chroma_nz, h_jhist_ + 6 * 256, 8);
   return true;
 }
 

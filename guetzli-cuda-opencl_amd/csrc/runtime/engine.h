@@ -203,6 +203,13 @@ class Engine {
                   const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change);
   bool OrderFetch(std::pair<int, float>* out, size_t n);
   bool OrderAdvance(float val_threshold, int direction);
+  // The back end's bulk prefix applied to the device copy (k_bulk_apply):
+  // cnt[b] changes of block b from the last_indexes of this iteration's
+  // OrderBuild, zeroed (direction 1) or restored to Quantize(orig, quant);
+  // then the histogram stage of the changed image (as JpegStage: hist,
+  // chroma_nz), waited for.
+  bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, uint32_t* hist,
+                 uint64_t* chroma_nz);
 
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
@@ -320,6 +327,8 @@ class Engine {
   void* h_ord_entries_ = nullptr;   // mapped pinned: the entries
   void* m_ord_entries_ = nullptr;
   size_t h_ord_entries_cap_ = 0;
+  uint8_t* h_bulk_ = nullptr;       // mapped pinned: BulkApply's per-block change counts
+  uint8_t* m_bulk_ = nullptr;
 };
 
 // Process-wide pool of idle engines keyed by (device, width, height): an
