@@ -870,10 +870,13 @@ struct ChangeLoop {
   // factor: the searched blocks' size in 8x8 blocks (4:2:0 chroma: 2);
   // *first_up_iter: the first up iteration's floor on min_coeffs (the count
   // of keys below 0.75 x the block error limit), then cleared.
+  // (n_total / below: the frame's entry count and count below the floor
+  // when `order` holds only this rank's entries; else taken from order)
   ChangeLoop(int direction, bool distance_ok, int base_size, int factor, int blocks_to_change,
              bool* first_up_iter, float block_error_limit,
-             const std::vector<std::pair<int, float>>& order)
-      : n_order(order.size()) {
+             const std::vector<std::pair<int, float>>& order, size_t n_total = SIZE_MAX,
+             int64_t below_floor = -1)
+      : n_order(n_total == SIZE_MAX ? order.size() : n_total) {
     double rel_size_delta = direction > 0 ? 0.01 : 0.0005;
     if (direction > 0 && distance_ok) rel_size_delta = 0.05;
     min_size_delta = base_size * rel_size_delta;
@@ -882,8 +885,11 @@ struct ChangeLoop {
     if (*first_up_iter) {
       const float limit = 0.75f * block_error_limit;
       // partition_point(key < limit) of the sorted order == count of keys below limit
-      int below = 0;
-      for (const auto& e : order) below += e.second < limit ? 1 : 0;
+      int below = static_cast<int>(below_floor);
+      if (below_floor < 0) {
+        below = 0;
+        for (const auto& e : order) below += e.second < limit ? 1 : 0;
+      }
       min_coeffs = std::max<int>(min_coeffs, below);
       *first_up_iter = false;
     }
@@ -1018,6 +1024,266 @@ size_t EntropyCodedDataSize(const std::vector<JpegHistogram>& histograms,
   for (size_t i = 0; i < histograms.size(); ++i)
     bits += HistogramEntropyCost(histograms[i], &depths[i * JpegHistogram::kSize]);
   return (bits + 7) / 8;
+}
+
+// The order of one back-end iteration's change entries on a frame split
+// over ranks (host/strips.h), from every rank's own entries.  std::sort
+// (processor.cc:840-843) is not stable, so where keys are equal its order
+// is that of libstdc++'s introsort over the frame's array -- the exact path
+// (LazyStdSort on every rank, after an all-gather of every entry).  But the
+// loop consumes a prefix as a set and then a short tail in order, and those
+// are functions of the keys alone wherever no key is shared by entries of
+// two blocks (entries of one block are interchangeable: a change takes the
+// block's next candidate, whichever entry named it).  So:
+//   * Prefix: the bulk-th smallest key K* by a radix selection over every
+//     rank's keys (three small all-sums of bucket counts); the prefix is
+//     every key below K* plus the K*-keyed entries it reaches -- all of them,
+//     or some of one block's; K* shared by several blocks across the
+//     boundary leaves the set open (the caller takes the exact path);
+//   * Next: the tail in windows, each rank's next entries (smallest first)
+//     merged on every rank; a position is certified when no rank can still
+//     hold a smaller key, and a tie of several blocks among the certified
+//     entries ends the window there (open: the caller takes the exact path
+//     from that position on -- the positions before it are the same in
+//     std::sort's order).
+// No rank gathers or sorts the frame's entries unless a tie leaves the
+// order open.
+class StripOrder {
+ public:
+  // Order-preserving bits of a float key (equal keys -- both zeros -- give
+  // equal bits).
+  static uint32_t Bits(float k) {
+    if (k == 0.0f) return 0x80000000u;
+    uint32_t u;
+    std::memcpy(&u, &k, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  }
+
+  // cnt (num_blocks, local indices) := per owned block its entries among the
+  // first `bulk` of the frame's order.  1: done; 0: open; -1: failed exchange.
+  int Prefix(const std::vector<std::pair<int, float>>& local, size_t bulk, Partition* part, int gbase,
+             int num_blocks, std::vector<int>* cnt) {
+    // radix selection of the key of rank bulk - 1: 12 + 12 + 8 bits
+    static const int kShift[3] = {20, 8, 0}, kBits[3] = {12, 12, 8};
+    uint32_t prefix = 0;
+    int64_t below = 0, eq = 0;
+    const int64_t target = static_cast<int64_t>(bulk) - 1;
+    for (int round = 0; round < 3; ++round) {
+      const int sh = kShift[round], nb = kBits[round];
+      std::vector<int64_t> h(static_cast<size_t>(1) << nb, 0);
+      const int hi_sh = sh + nb;
+      for (const auto& e : local) {
+        const uint32_t u = Bits(e.second);
+        if (hi_sh < 32 && (u >> hi_sh) != prefix) continue;
+        ++h[(u >> sh) & ((1u << nb) - 1)];
+      }
+      if (!part->SumAll(h.data(), static_cast<int>(h.size()))) return -1;
+      int64_t cum = below;
+      uint32_t j = 0;
+      for (; j + 1 < h.size() && cum + h[j] <= target; ++j) cum += h[j];
+      below = cum;
+      eq = h[j];
+      prefix = (prefix << nb) | j;
+    }
+    kbits_ = prefix;
+    tie_block_ = -1;
+    take_ = 0;
+    if (TestOpen() == 1) return 0;
+    if (below + eq > static_cast<int64_t>(bulk)) {
+      // K* straddles the boundary: determined only if one block holds every
+      // entry keyed K* (local entries are in block order)
+      std::vector<uint8_t> mine;
+      int last = -1;
+      for (const auto& e : local)
+        if (Bits(e.second) == kbits_ && e.first != last) {
+          last = e.first;
+          mine.insert(mine.end(), reinterpret_cast<const uint8_t*>(&last),
+                      reinterpret_cast<const uint8_t*>(&last) + 4);
+        }
+      std::vector<std::vector<uint8_t>> all;
+      if (!part->coll->AllGatherV(mine, &all)) return -1;
+      size_t blocks = 0;
+      for (const auto& m : all) {
+        blocks += m.size() / 4;
+        if (m.size() >= 4) std::memcpy(&tie_block_, m.data(), 4);
+      }
+      if (blocks != 1) return 0;
+      take_ = static_cast<int64_t>(bulk) - below;
+    }
+    cnt->assign(num_blocks, 0);
+    for (const auto& e : local) {
+      const uint32_t u = Bits(e.second);
+      if (u < kbits_ || (u == kbits_ && tie_block_ < 0)) ++(*cnt)[e.first - gbase];
+    }
+    if (tie_block_ >= 0 && tie_block_ - gbase >= 0 && tie_block_ - gbase < num_blocks) {
+      // (only the owner has entries of it; a halo block is never searched here)
+      bool owner = false;
+      for (const auto& e : local) owner = owner || e.first == tie_block_;
+      if (owner) (*cnt)[tie_block_ - gbase] += static_cast<int>(take_);
+    }
+    have_prefix_ = true;
+    return 1;
+  }
+
+  // This rank's entries after the prefix (all, without one), for Next.
+  void StartTail(const std::vector<std::pair<int, float>>& local, bool after_prefix) {
+    rem_.clear();
+    int64_t skip = take_;
+    for (const auto& e : local) {
+      const uint32_t u = Bits(e.second);
+      if (after_prefix) {
+        if (u < kbits_) continue;
+        if (u == kbits_) {
+          if (tie_block_ < 0) continue;   // all K*-keyed entries are in the prefix
+          if (skip > 0) {                 // the prefix's share of tie_block_'s
+            --skip;
+            continue;
+          }
+        }
+      }
+      rem_.push_back(Entry{u, e.first, e.second});
+    }
+    pos_ = 0;
+    sorted_ = 0;
+    static const size_t kFirst = [] {
+      const char* w = std::getenv("GZ_STRIP_WINDOW");  // (tests: small windows)
+      return static_cast<size_t>(w && std::atoi(w) > 0 ? std::atoi(w) : 1024);
+    }();
+    window_ = kFirst;
+  }
+
+  // The next certified positions of the frame's order.  *open: the position
+  // after them starts a tie of several blocks.  1: ok; 0: every rank's
+  // entries are consumed; -1: failed exchange.
+  int Next(Partition* part, std::vector<int>* blocks, std::vector<float>* keys, bool* open) {
+    *open = false;
+    for (;;) {
+      const size_t k = std::min(window_, rem_.size() - pos_);
+      if (pos_ + k > sorted_) {
+        // the smallest entries left, sorted, a good way ahead of the window
+        const size_t want = std::min(rem_.size(), pos_ + std::max<size_t>(4 * k, 1 << 16));
+        auto less = [](const Entry& a, const Entry& b) {
+          return a.bits != b.bits ? a.bits < b.bits : a.block < b.block;
+        };
+        if (want < rem_.size()) std::nth_element(rem_.begin() + pos_, rem_.begin() + want, rem_.end(), less);
+        std::sort(rem_.begin() + pos_, rem_.begin() + want, less);
+        sorted_ = want;
+      }
+      std::vector<uint8_t> send(1 + 12 * k);
+      send[0] = pos_ + k < rem_.size() ? 1 : 0;
+      for (size_t i = 0; i < k; ++i) {
+        const Entry& e = rem_[pos_ + i];
+        std::memcpy(&send[1 + 12 * i], &e.bits, 4);
+        std::memcpy(&send[5 + 12 * i], &e.block, 4);
+        std::memcpy(&send[9 + 12 * i], &e.key, 4);
+      }
+      std::vector<std::vector<uint8_t>> all;
+      if (!part->coll->AllGatherV(send, &all)) return -1;
+      uint64_t bound = uint64_t{1} << 32;
+      size_t sent = 0;
+      for (const auto& m : all) {
+        if (m.empty() || (m.size() - 1) % 12) return -1;
+        const size_t n = (m.size() - 1) / 12;
+        sent += n;
+        if (m[0] && n) {
+          uint32_t b;
+          std::memcpy(&b, &m[1 + 12 * (n - 1)], 4);
+          bound = std::min<uint64_t>(bound, b);
+        }
+      }
+      if (sent == 0) return 0;
+      struct M {
+        uint32_t bits;
+        int rank;
+        size_t idx;
+        int block;
+        float key;
+      };
+      std::vector<M> merged;
+      for (int r = 0; r < static_cast<int>(all.size()); ++r) {
+        const auto& m = all[r];
+        for (size_t i = 0; i < (m.size() - 1) / 12; ++i) {
+          M x{0, r, i, 0, 0.0f};
+          std::memcpy(&x.bits, &m[1 + 12 * i], 4);
+          std::memcpy(&x.block, &m[5 + 12 * i], 4);
+          std::memcpy(&x.key, &m[9 + 12 * i], 4);
+          if (x.bits < bound) merged.push_back(x);
+        }
+      }
+      if (merged.empty()) {  // every sent key at the bound: wider windows
+        window_ *= 2;
+        continue;
+      }
+      std::sort(merged.begin(), merged.end(), [](const M& a, const M& b) {
+        return a.bits != b.bits ? a.bits < b.bits : (a.rank != b.rank ? a.rank < b.rank : a.idx < b.idx);
+      });
+      // the first tie of several blocks ends the certified positions at its group's start
+      size_t end = merged.size();
+      for (size_t t = 1; t < merged.size(); ++t)
+        if (merged[t].bits == merged[t - 1].bits && merged[t].block != merged[t - 1].block) {
+          size_t g = t - 1;
+          while (g > 0 && merged[g - 1].bits == merged[t].bits) --g;
+          end = g;
+          *open = true;
+          break;
+        }
+      if (TestOpen() == 2 && end > 1) {  // (tests: the fallback in mid-tail)
+        end /= 2;
+        *open = true;
+      }
+      const int me = part->rank;
+      blocks->clear();
+      keys->clear();
+      mine_.clear();
+      for (size_t t = 0; t < end; ++t) {
+        blocks->push_back(merged[t].block);
+        keys->push_back(merged[t].key);
+        mine_.push_back(merged[t].rank == me ? 1 : 0);
+      }
+      return 1;
+    }
+  }
+
+  // GZ_STRIP_TEST_OPEN=prefix / tail: report the prefix / the middle of the
+  // first tail window as open, so that tests take the exact path from there
+  // (the result must not change).
+  static int TestOpen() {
+    static const int v = [] {
+      const char* e = std::getenv("GZ_STRIP_TEST_OPEN");
+      if (!e) return 0;
+      return std::strcmp(e, "prefix") == 0 ? 1 : std::strcmp(e, "tail") == 0 ? 2 : 0;
+    }();
+    return v;
+  }
+
+  // The caller processed the first n positions of the last window.
+  void Consumed(size_t n) {
+    for (size_t t = 0; t < n && t < mine_.size(); ++t) pos_ += mine_[t];
+    window_ = std::min<size_t>(window_ * 2, size_t{1} << 16);
+  }
+
+ private:
+  struct Entry {
+    uint32_t bits;
+    int block;
+    float key;
+  };
+  uint32_t kbits_ = 0;
+  bool have_prefix_ = false;
+  int tie_block_ = -1;
+  int64_t take_ = 0;
+  std::vector<Entry> rem_;
+  size_t pos_ = 0, sorted_ = 0, window_ = 1024;
+  std::vector<uint8_t> mine_;
+};
+
+// GZ_STRIP_ORDER=exact: every iteration on the exact path (A/B and tests).
+bool StripFastOrder() {
+  static const bool fast = [] {
+    const char* e = std::getenv("GZ_STRIP_ORDER");
+    return !(e && std::strcmp(e, "exact") == 0);
+  }();
+  return fast;
 }
 
 class Processor {
@@ -1157,7 +1423,7 @@ class Processor {
                         const std::vector<int>& last_indexes, const std::vector<int>& offsets,
                         const std::vector<float>& cand_err, const std::vector<float>& max_block_error,
                         std::vector<std::pair<int, float>>* order, std::vector<float>* block_weight,
-                        int* blocks_to_change);
+                        int* blocks_to_change, size_t* frame_entries = nullptr);
   // The 4:2:0 pass (processor.cc:989-1016, downsample = 1) on the host model
   // Image420, entropy coded on the host.
   int Run420(const JpegData& jpg_in, std::string* err);
@@ -1181,6 +1447,7 @@ class Processor {
   double encode_s_ = 0.0;
   double final_score_ = -1;
   std::vector<int> bulk_cnt_;  // per-block change counts of a back-end bulk prefix
+  StripOrder strip_order;      // (a frame split over ranks)
   static constexpr int kOrderChunk = 1024;     // blocks per parallel back-end work item
   static constexpr size_t kMinBulkChanges = 64;
 };
@@ -1350,6 +1617,13 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       std::vector<std::pair<int, float>> global_order;
       int blocks_to_change = 0;
       std::vector<float> block_weight;
+      // A frame split over ranks: by default every rank keeps its own
+      // entries (StripOrder below) and the frame's std::sort order is
+      // derived from them where the consumed entries' keys decide it alone;
+      // strip_exact: the whole frame's entries on every rank (the fallback).
+      bool strip_exact = part_ && part_->world > 1 && !StripFastOrder();
+      const bool strip_fast = part_ && part_->world > 1 && !strip_exact;
+      size_t frame_n = 0;
       if (device_order) {
         if (!cmp_->DeviceChangeOrder(direction, target_mul, first_up_iter, last_indexes, &global_order,
                                      &blocks_to_change))
@@ -1357,21 +1631,41 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       } else if (!BuildChangeOrder(direction, 1, target_mul, num_blocks, own_lo, own_hi, gbase,
                                    first_up_iter ? zero_block_max : cmp_->block_max_distance(), last_indexes,
                                    offsets, cand_err, max_block_error, &global_order, &block_weight,
-                                   &blocks_to_change)) {
+                                   &blocks_to_change, strip_fast ? &frame_n : nullptr)) {
         return exchange_failed();
       }
+      if (!strip_fast) frame_n = global_order.size();
       res_->detail["backend_order_s"] += Since(tb);
-      res_->detail["backend_order_entries"] += static_cast<double>(global_order.size());
-      if (global_order.empty()) {
+      res_->detail["backend_order_entries"] += static_cast<double>(frame_n);
+      if (frame_n == 0) {
         res_->seconds_backend += Since(tb);
         break;
       }
       // std::sort(global_order) by key (processor.cc:840-843), materialised
       // lazily: only the prefix the change loop consumes gets sorted.
-      LazyStdSort sorter(global_order.data(), global_order.size());
+      std::unique_ptr<LazyStdSort> sorter;
+      if (!strip_fast) sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
+      // strip_fast: this rank's entries, global_order, become the frame's (the
+      // exact path) when their keys leave std::sort's order open
+      auto go_exact = [&]() -> bool {
+        int btc = blocks_to_change;
+        if (!GatherEntries(&global_order, own_lo, own_hi, gbase, &btc)) return false;
+        sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
+        strip_exact = true;
+        res_->detail["strip_order_fallbacks"] += 1;
+        return true;
+      };
       const auto tc = Clock::now();
+      // (the frame's count of keys below the first up iteration's floor)
+      int64_t below_floor = -1;
+      if (strip_fast && first_up_iter) {
+        const float limit = 0.75f * cmp_->BlockErrorLimit();
+        below_floor = 0;
+        for (const auto& e : global_order) below_floor += e.second < limit ? 1 : 0;
+        if (!part_->SumAll(&below_floor, 1)) return exchange_failed();
+      }
       ChangeLoop loop(direction, cmp_->DistanceOK(1.0), base_size, 1, blocks_to_change, &first_up_iter,
-                      cmp_->BlockErrorLimit(), global_order);
+                      cmp_->BlockErrorLimit(), global_order, frame_n, below_floor);
       int est_jpg_size = prev_size;
       // Changes before the loop's first read of an entropy code or size
       // estimate (first_read: the first i % 10 == 0 step whose codes are
@@ -1384,7 +1678,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       size_t bulk = 0;
       {
         const long m = std::max(0, loop.min_coeffs);
-        const long n = static_cast<long>(global_order.size());
+        const long n = static_cast<long>(frame_n);
         const long lo = std::max(0L, std::min(m - 9, n - 10));
         const long first_code = (lo + 9) / 10 * 10;
         const long first_read = std::min(std::min(first_code, m), n - 1);
@@ -1392,12 +1686,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       }
       if (bulk) {
         const auto tbk = Clock::now();
-        sorter.SetPrefix(bulk);
+        if (strip_fast) {
+          // the prefix as a set from the keys alone (StripOrder::Prefix);
+          // open (tied keys of several blocks across its boundary): exact
+          const int r = strip_order.Prefix(global_order, bulk, part_, gbase, num_blocks, &bulk_cnt_);
+          if (r < 0) return exchange_failed();
+          if (r == 0 && !go_exact()) return exchange_failed();
+        }
+        if (!strip_fast || strip_exact) sorter->SetPrefix(bulk);
         res_->detail["backend_setprefix_s"] += Since(tbk);
         // per-block counts of the prefix's owned entries (parallel; blocks
         // are spread, so the atomic increments rarely meet)
+        if (!strip_fast || strip_exact) {
         bulk_cnt_.assign(num_blocks, 0);
-        {
           const int kSlices = bulk >= (size_t{1} << 18) ? 64 : 1;
           int* cnt = bulk_cnt_.data();
           ParallelFor(kSlices, [&](int sl) {
@@ -1518,14 +1819,14 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
         }
       }
-      const size_t n_order = global_order.size();
+      const size_t n_order = frame_n;
       double codes_s = 0.0;
       int n_codes = 0;
       double sort_s = 0.0;
       // one change's bookkeeping after it was applied: the decade's codes,
       // the estimate and the break test; true: stop after change i
-      auto after_change = [&](size_t i) -> bool {
-        loop.Applied(global_order[i].second);
+      auto after_change = [&](size_t i, float key) -> bool {
+        loop.Applied(key);
         if (loop.CodesRead(i)) {
           const auto te = Clock::now();
           ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
@@ -1593,17 +1894,17 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           }
         };
         for (size_t i = bulk; i < n_order; ++i) {
-          if (i >= sorter.sorted()) {
+          if (i >= sorter->sorted()) {
             const auto ts = Clock::now();
-            sorter.EnsureSorted(i);
+            sorter->EnsureSorted(i);
             sort_s += Since(ts);
           }
           if (i >= prefetched) {
-            prefetched = std::max(sorter.sorted(), i + 1);
+            prefetched = std::max(sorter->sorted(), i + 1);
             prefetch_chunk(i, std::min(prefetched, n_order));
           }
           apply(global_order[i].first, nullptr);
-          if (after_change(i)) break;
+          if (after_change(i, global_order[i].second)) break;
         }
       } else {
         // The tail on a partitioned frame, a window of entries at a time: the
@@ -1617,29 +1918,23 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           uint64_t nz;
         };
         std::vector<Undo> undo;
-        size_t window = 4096;
-        size_t i = bulk;
-        bool stop = false;
-        while (!stop && i < n_order) {
-          const size_t W = std::min(window, n_order - i);
-          if (i + W > sorter.sorted()) {
-            const auto ts = Clock::now();
-            sorter.EnsureSorted(i + W - 1);
-            sort_s += Since(ts);
-          }
+        // the window of order positions i0 .. i0 + W - 1 (frame blocks /
+        // keys); *done: positions processed (through the break if *stop)
+        auto tail_window = [&](const int* blocks, const float* keys, size_t W, size_t i0, bool* stop,
+                               size_t* done) -> bool {
           std::vector<uint8_t> rec;
           undo.clear();
-          for (size_t j = i; j < i + W; ++j) {
-            const int bix = global_order[j].first - gbase;
+          for (size_t j = 0; j < W; ++j) {
+            const int bix = blocks[j] - gbase;
             if (bix < own_lo || bix >= own_hi) continue;
             const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
             const int idx = cand[off + last_indexes[bix] + std::min(direction, 0)];
             const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
-            undo.push_back(Undo{j, bix, c, k, img->block(c, bix)[k],
+            undo.push_back(Undo{i0 + j, bix, c, k, img->block(c, bix)[k],
                                 acm.nz[static_cast<size_t>(c) * num_blocks + bix]});
             SymbolLog log;
             apply(bix, &log);
-            const uint32_t pos = static_cast<uint32_t>(j - i);
+            const uint32_t pos = static_cast<uint32_t>(j);
             rec.insert(rec.end(), reinterpret_cast<const uint8_t*>(&pos),
                        reinterpret_cast<const uint8_t*>(&pos) + 4);
             rec.push_back(static_cast<uint8_t>(c));
@@ -1651,40 +1946,86 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           }
           const auto tx = Clock::now();
           std::vector<std::vector<uint8_t>> all;
-          if (!part_->coll->AllGatherV(rec, &all)) return exchange_failed();
+          if (!part_->coll->AllGatherV(rec, &all)) return false;
           res_->detail["strip_tail_exchange_s"] += Since(tx);
           std::vector<const uint8_t*> at(W, nullptr);
           for (const auto& m : all)
             for (const uint8_t* p = m.data(); p < m.data() + m.size();) {
               uint32_t pos;
               std::memcpy(&pos, p, 4);
-              if (pos >= W) return exchange_failed();
+              if (pos >= W) return false;
               at[pos] = p + 4;
               p += 6 + 2 * p[5];
             }
-          size_t j = i;
-          for (; j < i + W; ++j) {
-            const uint8_t* r = at[j - i];
-            if (!r) return exchange_failed();
+          size_t j = 0;
+          for (; j < W; ++j) {
+            const uint8_t* r = at[j];
+            if (!r) return false;
             const int c = r[0];
             for (int e = 0; e < r[1]; ++e) {
               const int sym = r[2 + 2 * e], w = static_cast<int8_t>(r[3 + 2 * e]);
               ac_histograms[c].Add(sym, w);
               raw_bits[c] += static_cast<int64_t>(w) * (ac_depths[c * JpegHistogram::kSize + sym] + (sym & 0xf));
             }
-            if (after_change(j)) {
-              stop = true;
+            if (after_change(i0 + j, keys[j])) {
+              *stop = true;
               break;
             }
           }
-          if (stop) {
-            for (auto u = undo.rbegin(); u != undo.rend() && u->i > j; ++u) {
+          if (*stop) {
+            for (auto u = undo.rbegin(); u != undo.rend() && u->i > i0 + j; ++u) {
               img->block(u->c, u->bix)[u->k] = u->old;
               acm.nz[static_cast<size_t>(u->c) * num_blocks + u->bix] = u->nz;
               last_indexes[u->bix] -= direction;
             }
           }
-          i = stop ? j + 1 : i + W;
+          *done = *stop ? j + 1 : W;
+          return true;
+        };
+        size_t i = bulk;
+        bool stop = false;
+        if (strip_fast && !strip_exact) {
+          // windows of the frame's order merged from every rank's next
+          // entries (StripOrder::Next); positions whose entry the keys leave
+          // open (a tie of several blocks) switch to the exact order
+          strip_order.StartTail(global_order, bulk > 0);
+          while (!stop && i < n_order) {
+            std::vector<int> blocks;
+            std::vector<float> keys;
+            bool open = false;
+            const int r = strip_order.Next(part_, &blocks, &keys, &open);
+            if (r < 0) return exchange_failed();
+            if (r == 0) break;  // (no entries left on any rank)
+            size_t done = 0;
+            const size_t W = std::min(blocks.size(), n_order - i);
+            if (W && !tail_window(blocks.data(), keys.data(), W, i, &stop, &done)) return exchange_failed();
+            strip_order.Consumed(done);
+            i += done;
+            if (!stop && open) {
+              if (!go_exact()) return exchange_failed();
+              if (bulk) sorter->SetPrefix(bulk);
+              break;
+            }
+          }
+          res_->detail["strip_order_fast_iters"] += strip_exact ? 0 : 1;
+        }
+        size_t window = 4096;
+        while ((!strip_fast || strip_exact) && !stop && i < n_order) {
+          const size_t W = std::min(window, n_order - i);
+          if (i + W > sorter->sorted()) {
+            const auto ts = Clock::now();
+            sorter->EnsureSorted(i + W - 1);
+            sort_s += Since(ts);
+          }
+          std::vector<int> blocks(W);
+          std::vector<float> keys(W);
+          for (size_t j = 0; j < W; ++j) {
+            blocks[j] = global_order[i + j].first;
+            keys[j] = global_order[i + j].second;
+          }
+          size_t done = 0;
+          if (!tail_window(blocks.data(), keys.data(), W, i, &stop, &done)) return exchange_failed();
+          i += done;
           window *= 2;
         }
       }
@@ -1722,7 +2063,8 @@ bool Processor::BuildChangeOrder(int direction, int factor, double target_mul, i
                                  const std::vector<float>& cand_err,
                                  const std::vector<float>& max_block_error,
                                  std::vector<std::pair<int, float>>* order,
-                                 std::vector<float>* block_weight, int* blocks_to_change) {
+                                 std::vector<float>* block_weight, int* blocks_to_change,
+                                 size_t* frame_entries) {
   const int own_chunks = (own_hi - own_lo + kOrderChunk - 1) / kOrderChunk;
   const int cand_n = static_cast<int>(cand_err.size());
   std::vector<float>& weight = *block_weight;
@@ -1776,6 +2118,15 @@ bool Processor::BuildChangeOrder(int direction, int factor, double target_mul, i
         }
       }
     });
+    if (part_ && part_->world > 1 && frame_entries) {
+      // this rank's entries only (StripOrder); the frame's totals
+      int64_t t[2] = {static_cast<int64_t>(order->size()), *blocks_to_change};
+      if (!part_->SumAll(t, 2)) return false;
+      *frame_entries = static_cast<size_t>(t[0]);
+      *blocks_to_change = static_cast<int>(t[1]);
+      if (t[0] > 0) break;
+      continue;
+    }
     if (part_ && part_->world > 1) {
       // the frame's order: every rank's entries in rank (= block) order; a
       // rank sends its keys and a count per owned block

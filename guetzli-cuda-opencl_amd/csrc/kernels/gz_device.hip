@@ -448,7 +448,6 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
   const size_t stage_groups = (3 * static_cast<size_t>(e->nb_) + kStageBlocks - 1) / kStageBlocks;
   alloc(reinterpret_cast<void**>(&e->d_jhist_), jhist_device_bytes(stage_groups));
-  alloc(&e->d_jcodes_, sizeof(JpegCodesPacked));
   // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
   e->jwords_cap_ = static_cast<size_t>(e->nb_) * 160 + 16;
   alloc(reinterpret_cast<void**>(&e->d_jwords_[0]), e->jwords_cap_ * 4);
@@ -462,14 +461,15 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_jhist_), e->h_jhist_, 0) != hipSuccess)
     ok = false;
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jcodes_), sizeof(JpegCodesPacked)) != hipSuccess)
-    ok = false;
   if (ok && (hipMemsetAsync(e->d_jhist_, 0, jhist_device_bytes(stage_groups), s) != hipSuccess ||
              hipMemsetAsync(e->d_jctl_, 0, jctl_bytes, s) != hipSuccess))
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4) != hipSuccess)
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4 + 16, hipHostMallocCoherent) !=
+                hipSuccess)
+    ok = false;
+  if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_block_max_), e->h_block_max_, 0) != hipSuccess)
     ok = false;
   if (!ok) return fail("device allocation failed");
   // pinned staging (coefficients, offsets, histograms, block maxima)
@@ -604,7 +604,7 @@ Engine::~Engine() {
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
-                  d_jmask_, d_jhist_, d_jcodes_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
+                  d_jmask_, d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -616,7 +616,6 @@ Engine::~Engine() {
   if (h_zero_off_) hipHostFree(h_zero_off_);
   if (h_coeffs_) hipHostFree(h_coeffs_);
   if (h_jhist_) hipHostFree(h_jhist_);
-  if (h_jcodes_) hipHostFree(h_jcodes_);
   if (h_bulk_) (void)hipHostFree(h_bulk_);
   if (h_jbytes_) hipHostFree(h_jbytes_);
   if (h_cand_idx_) hipHostFree(h_cand_idx_);
@@ -898,7 +897,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
-                                                              dm, d_block_max_));
+                                                              dm, d_block_max_, m_block_max_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");
@@ -910,7 +909,6 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
   GZ_HIP(hipSetDevice(device_));
   if (dbg) {
     if (!EnqueueCompare(dbg)) return false;
-    GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
   } else if (!CompareEnqueue()) {
     return false;
   }
@@ -944,7 +942,7 @@ bool Engine::CompareEnqueue() {
     }
     GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graph), s));
   }
-  GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, nb_ * 4, hipMemcpyDeviceToHost, s));
+  // (the block maxima reach h_block_max_ from k_diffmap_final itself)
   return true;
 }
 
@@ -1477,13 +1475,20 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
   if (m0 < 0 || m1 > nb_ || m1 <= m0) return Fail("JpegScan block range", 0);
-  for (int c = 0; c < 3; ++c)
+  JpegCodesArg dc;
+  for (int c = 0; c < 3; ++c) {
     for (int i = 0; i < 256; ++i) {
-      h_jcodes_->e[c][i] = (static_cast<uint32_t>(codes.dc_len[c][i]) << 16) | codes.dc_code[c][i];
-      h_jcodes_->e[c][256 + i] = (static_cast<uint32_t>(codes.ac_len[c][i]) << 16) | codes.ac_code[c][i];
+      if (i >= kJDcSyms && codes.dc_len[c][i]) return Fail("JpegScan DC category above 16", 0);
+      if (i < kJDcSyms) {
+        dc.dc[c][i][0] = static_cast<uint8_t>(codes.dc_code[c][i]);
+        dc.dc[c][i][1] = static_cast<uint8_t>(codes.dc_code[c][i] >> 8);
+        dc.dc[c][i][2] = codes.dc_len[c][i];
+      }
+      dc.ac[c][i][0] = static_cast<uint8_t>(codes.ac_code[c][i]);
+      dc.ac[c][i][1] = static_cast<uint8_t>(codes.ac_code[c][i] >> 8);
+      dc.ac[c][i][2] = codes.ac_len[c][i];
     }
-  GZ_HIP(hipMemcpyAsync(d_jcodes_, h_jcodes_, sizeof(JpegCodesPacked), hipMemcpyHostToDevice, s));
-  const JpegCodesPacked* dc = static_cast<const JpegCodesPacked*>(d_jcodes_);
+  }
   // (the bits of an MCU are bounded by its 3 blocks: the capacity holds any
   // scan of these MCUs, plus the word of an unaligned start)
   uint32_t* words = d_jwords_[jslot_];

@@ -22,15 +22,8 @@ struct CoeffDataHost {  // guetzli::CoeffData (processor.h:29-32)
   float block_err;
 };
 
-// Optional host destinations for stage-level parity tests.
 // Per component Huffman code (length, code) of every symbol, as the device
 // entropy coder consumes them.
-// The same codes as the device reads them: (length << 16) | code per
-// symbol, e[comp][0..255] DC, e[comp][256..511] AC (one load per lookup).
-struct JpegCodesPacked {
-  uint32_t e[3][512];
-};
-
 struct JpegCodeTables {
   uint8_t dc_len[3][256];
   uint8_t ac_len[3][256];
@@ -38,6 +31,7 @@ struct JpegCodeTables {
   uint16_t ac_code[3][256];
 };
 
+// Optional host destinations for stage-level parity tests.
 struct CompareDebug {
   float* cand_linear = nullptr;   // 3*w*h
   float* cand_xyb = nullptr;      // 3*w*h
@@ -286,7 +280,6 @@ class Engine {
   int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
   uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
   uint32_t* d_jhist_ = nullptr;    //   kJHistCopies x 6 x 256 counts + chroma non-zeros (u64) + done counter
-  void* d_jcodes_ = nullptr;       //   JpegCodesPacked
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
   ScanPart jpart_[2];
@@ -296,7 +289,6 @@ class Engine {
   size_t jwords_cap_ = 0;
   uint32_t* h_jhist_ = nullptr;    // pinned: counts + chroma + (0xff count, total bits),
   uint32_t* m_jhist_ = nullptr;    //   written by the kernels through this mapped address
-  JpegCodesPacked* h_jcodes_ = nullptr;
   uint8_t* h_jbytes_ = nullptr;
   size_t h_jbytes_cap_ = 0;
   int* h_zero_off_ = nullptr;      // pinned
@@ -313,7 +305,8 @@ class Engine {
   size_t cbreq_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
-  float* h_block_max_ = nullptr;
+  float* h_block_max_ = nullptr;   // mapped: k_diffmap_final writes the block maxima here too
+  float* m_block_max_ = nullptr;
   // device change order (allocated on first use): weight f32 | active i32 |
   // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
   // max_block_error f32 | last_indexes i32

@@ -90,6 +90,7 @@ int main(int argc, char** argv) {
   Exchange x(world);
   std::vector<std::string> out(world), errs(world);
   std::vector<int> rc(world, -1), iters(world, 0);
+  std::vector<double> fast_iters(world, 0.0), fallbacks(world, 0.0);
   std::vector<std::thread> ranks;
   for (int r = 0; r < world; ++r) {
     ranks.emplace_back([&, r] {
@@ -108,6 +109,8 @@ int main(int argc, char** argv) {
       rc[r] = gz::ProcessJpegData(params, jpg, &cmp, &res, &errs[r], &part);
       out[r] = res.jpeg;
       iters[r] = res.iterations;
+      fast_iters[r] = res.detail["strip_order_fast_iters"];
+      fallbacks[r] = res.detail["strip_order_fallbacks"];
     });
   }
   for (auto& t : ranks) t.join();
@@ -131,6 +134,11 @@ int main(int argc, char** argv) {
   FILE* o = fopen(argv[6], "wb");
   fwrite(out[0].data(), 1, out[0].size(), o);
   fclose(o);
-  printf("{\"bytes\": %zu, \"iters\": %d, \"world\": %d}\n", out[0].size(), iters[0], world);
+  // (the back end's iterations whose order came from the ranks' own entries
+  // alone, and those that fell back to the exact order: host/processor.cc
+  // StripOrder)
+  printf("{\"bytes\": %zu, \"iters\": %d, \"world\": %d, \"strip_order_fast_iters\": %d, "
+         "\"strip_order_fallbacks\": %d}\n",
+         out[0].size(), iters[0], world, static_cast<int>(fast_iters[0]), static_cast<int>(fallbacks[0]));
   return 0;
 }

@@ -93,19 +93,41 @@ def test_oracle_strip_equals_full_image_on_owned_rows(gz, w, h, world, seed):
         assert np.array_equal(dc[:, y0 - e0:y1 - e0], full_dc[:, y0:y1])
 
 
+# The back end's order on a split frame (host/processor.cc StripOrder):
+# from the ranks' own entries (default; tiny merge windows), every iteration
+# exact (the whole frame's entries on every rank), and the switch to the
+# exact order forced at the prefix / in mid-tail.
+STRIP_ORDER_MODES = {
+    "fast": {},
+    "fast_window2": {"GZ_STRIP_WINDOW": "2"},
+    "exact": {"GZ_STRIP_ORDER": "exact"},
+    "open_prefix": {"GZ_STRIP_TEST_OPEN": "prefix"},
+    "open_tail": {"GZ_STRIP_TEST_OPEN": "tail", "GZ_STRIP_WINDOW": "3"},
+}
+
+
+@pytest.mark.parametrize("mode", sorted(STRIP_ORDER_MODES))
 @pytest.mark.parametrize("name,world", [("bees_q95", 2), ("bees_q84", 3)])
-def test_strip_comparator_threads_reproduce_reference(strips_e2e_bin, name, world, tmp_path):
+def test_strip_comparator_threads_reproduce_reference(strips_e2e_bin, name, world, mode, tmp_path):
     """StripComparator (product host code) with oracle strip comparators:
-    every rank's bytes equal the reference `guetzli --c` known answer."""
+    every rank's bytes equal the reference `guetzli --c` known answer, in
+    every mode of the back end's order."""
     e = MANIFEST["e2e"][name]
     out = tmp_path / "out.jpg"
+    env = dict(os.environ, **STRIP_ORDER_MODES[mode])
     res = subprocess.run([strips_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]),
                           str(e["h"]), str(e["quality"]), str(world), str(out)],
-                         capture_output=True, text=True, timeout=600)
+                         capture_output=True, text=True, timeout=600, env=env)
     assert res.returncode == 0, res.stderr
     info = json.loads(res.stdout)
     assert info["iters"] == e["iters"]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+    if mode.startswith("fast"):
+        assert info["strip_order_fast_iters"] > 0 and info["strip_order_fallbacks"] == 0, info
+    elif mode == "exact":
+        assert info["strip_order_fast_iters"] == 0 and info["strip_order_fallbacks"] == 0, info
+    else:
+        assert info["strip_order_fallbacks"] > 0, info
 
 
 @pytest.mark.parametrize("kind,at", [("compare", 1), ("compare", 5), ("zeroing", 1)])
