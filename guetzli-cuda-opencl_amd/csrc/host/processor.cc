@@ -2236,6 +2236,31 @@ void RemoveOriginalQuantization(JpegData* jpg, int q_in[3][kDCTBlockSize]) {
 }
 
 // IsGrayscale, processor.cc:921-929
+// The 4:4:4 JpegData of a 4:2:0 one whose chroma is all zero: Y cropped to
+// the image's blocks (a 4:2:0 file pads it to whole 16-pixel MCUs), chroma
+// zero at full resolution.
+JpegData Gray444Of420(const JpegData& jpg) {
+  JpegData g = jpg;
+  const int bw = (jpg.width + 7) / 8, bh = (jpg.height + 7) / 8;
+  g.max_h_samp_factor = g.max_v_samp_factor = 1;
+  g.mcu_cols = bw;
+  g.mcu_rows = bh;
+  for (int c = 0; c < 3; ++c) {
+    JpegComponent& comp = g.components[c];
+    comp.h_samp_factor = comp.v_samp_factor = 1;
+    comp.width_in_blocks = bw;
+    comp.height_in_blocks = bh;
+    comp.coeffs.assign(static_cast<size_t>(bw) * bh * kDCTBlockSize, 0);
+    if (c != 0) continue;
+    const JpegComponent& y = jpg.components[0];
+    for (int by = 0; by < bh; ++by)
+      std::memcpy(&comp.coeffs[static_cast<size_t>(by) * bw * kDCTBlockSize],
+                  &y.coeffs[static_cast<size_t>(by) * y.width_in_blocks * kDCTBlockSize],
+                  static_cast<size_t>(bw) * kDCTBlockSize * sizeof(coeff_t));
+  }
+  return g;
+}
+
 bool IsGrayscale(const JpegData& jpg) {
   for (int c = 1; c < 3; ++c)
     for (coeff_t v : jpg.components[c].coeffs)
@@ -2299,6 +2324,12 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
     return GZ_ERR_DEVICE;
   };
   CoeffImage img;
+  // A 4:2:0 input whose chroma is all zero: DownsampleImage leaves it and
+  // SaveToJpegData keeps its one component (processor.cc:990-1016), so its
+  // search is the grayscale pass below on the 4:4:4 image it equals (zero
+  // chroma upsamples to the same pixels at either factor)
+  const bool gray420 = input_is_420 && IsGrayscale(jpg);
+  JpegData jpg444;
   if (!input_is_420) {
     if (!cmp_->SetOriginalCoeffs(jpg)) return device_error();
     img.Init(jpg.width, jpg.height);
@@ -2341,21 +2372,27 @@ int Processor::Run(const JpegData& jpg_in, std::string* err) {
   // the "4:2:0" pass of such an image is the 4:4:4 machinery on a
   // one-component JpegData: the downsampling quantization generator, then the
   // Y search alone with ymul 1.0 (processor.cc:994-1016).
-  const bool gray_pass = !input_is_420 && IsGrayscale(jpg);
+  const bool gray_pass = (!input_is_420 || gray420) && IsGrayscale(jpg);
+  if (gray420) {  // (after the 4:2:0 Compare of the input above)
+    jpg444 = Gray444Of420(jpg);
+    if (!cmp_->SetOriginalCoeffs(jpg444)) return device_error();
+    img.Init(jpg.width, jpg.height);
+  }
   for (int downsample = force_420; downsample <= try_420; ++downsample) {
     if (downsample && !gray_pass) {
       const int rc = Run420(jpg_in, err);
       if (rc != GZ_OK) return rc;
       continue;
     }
+    const JpegData& src = gray420 ? jpg444 : jpg;
     JpegData gray;
-    const JpegData* pass_jpg = &jpg;
+    const JpegData* pass_jpg = &src;
     if (downsample) {
-      gray = jpg;
+      gray = src;
       gray.components.resize(1);
       pass_jpg = &gray;
     }
-    img.CopyFromJpegData(jpg);
+    img.CopyFromJpegData(src);
     int best_q[3][kDCTBlockSize];
     std::memcpy(best_q, q_in, sizeof(best_q));
     bool ok = false;

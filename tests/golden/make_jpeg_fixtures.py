@@ -69,6 +69,15 @@ def inputs():
     buf = io.BytesIO()
     Image.fromarray(np.ascontiguousarray(bees[:120, :160, 1])).save(buf, "JPEG", quality=85)
     out["gray1_pil_q85"] = (buf.getvalue(), 95)
+    # 4:2:0 with all-zero chroma (YCbCr given directly: Cb = Cr = 128, no
+    # colour conversion, so every chroma coefficient is 0): the reference
+    # keeps one component and searches Y alone (processor.cc:990-1016)
+    ycc = np.zeros((120, 160, 3), np.uint8)
+    ycc[..., 0] = bees[:120, :160, 1]
+    ycc[..., 1:] = 128
+    buf = io.BytesIO()
+    Image.fromarray(ycc, mode="YCbCr").save(buf, "JPEG", quality=85, subsampling=2)
+    out["gray420_pil_q85"] = (buf.getvalue(), 95)
     # a guetzli output as input (SOF1, guetzli's own table layout)
     tmp = tempfile.mkdtemp()
     raw = os.path.join(tmp, "bees88.rgb")
