@@ -275,7 +275,7 @@ bool DeviceEncodeJpeg(Engine* e, int w, int h, const int q[3][kDCTBlockSize], co
     return false;
   }
   uint64_t nbits = 0, ff = 0;
-  if (!e->JpegScan(ncomp, codes, &nbits, &ff)) {
+  if (!e->JpegScan(ncomp, q, codes, &nbits, &ff)) {
     if (err) *err = e->error();
     return false;
   }
@@ -398,7 +398,7 @@ bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const
   }
   seconds_encode += Since(t0);
   uint64_t nbits = 0, ff = 0;
-  if (!e->JpegScanEnqueue(ncomp, codes)) {
+  if (!e->JpegScanEnqueue(ncomp, img.quant, codes)) {
     err_ = e->error();
     return false;
   }
@@ -612,9 +612,59 @@ bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direct
     err_ = engine_->error();
     return false;
   }
-  JpegHistogram dc[3];
-  HistogramsFromStage(hist, chroma, dc, ac);
+  for (int c = 0; c < 3; ++c) {  // (every component: the back end's convention)
+    ac[c].Clear();
+    for (int i = 0; i < 256; ++i) ac[c].counts[i] = 2 * hist[(2 * c + 1) * 256 + i];
+  }
+  (void)chroma;
   seconds_bulk += Since(t0);
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta,
+                                                           bool strip_metadata, const JpegHistogram dc[3],
+                                                           const JpegHistogram ac[3], int ncomp,
+                                                           size_t* size) {
+  // the Compare pass first; the codes on the host while it runs; the scan
+  // behind it; one wait
+  const auto t0 = Clock::now();
+  const double c0 = ThreadCpu();
+  if (!SyncCoeffs(img)) return false;
+  Engine* e = engine_.get();
+  if (!e->CompareEnqueue()) {
+    err_ = e->error();
+    return false;
+  }
+  JpegHistogram dc_h[3], ac_h[3];
+  for (int c = 0; c < ncomp; ++c) {
+    dc_h[c] = dc[c];
+    ac_h[c] = ac[c];
+  }
+  JpegCodeTables codes;
+  if (!PrepareScan(w_, h_, img.quant, meta, strip_metadata, ncomp, dc_h, ac_h, &cur_prologue_, &codes)) {
+    err_ = "jpeg header";
+    return false;
+  }
+  seconds_encode += Since(t0);
+  uint64_t nbits = 0, ff = 0;
+  if (!e->JpegScanEnqueue(ncomp, img.quant, codes)) {
+    err_ = e->error();
+    return false;
+  }
+  const auto tw = Clock::now();
+  const double cw = ThreadCpu();
+  if (!e->Sync() || !e->JpegScanFinish(&nbits, &ff)) {
+    err_ = e->error();
+    return false;
+  }
+  seconds_wait += Since(tw);
+  cpu_wait += ThreadCpu() - cw;
+  e->CompareFinish(&distance_, block_max_.data());
+  ++compares;
+  cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
+  *size = cur_size_;
+  seconds_compare += Since(t0);
+  cpu_compare += ThreadCpu() - c0;
   return true;
 }
 
@@ -1362,6 +1412,35 @@ class Processor {
     res_->detail["encode_compare_s"] += Since(t0);
     return true;
   }
+  // EncodeAndCompare of a back-end candidate with its histograms known: the
+  // DC ones of the back end's start (DC coefficients do not change) and the
+  // tracked AC ones; the components SaveToJpegData keeps -- one when the
+  // chroma has become all zero (no chroma DC symbol but category 0, no
+  // chroma AC symbol with a magnitude) -- as the histogram pass would count.
+  bool EncodeAndCompareKnown(const JpegData& jpg, const CoeffImage& img, int saved0, const JpegHistogram dc0[3],
+                             const std::vector<JpegHistogram>& ac, std::string* err) {
+    FlushOutput();
+    const auto t0 = Clock::now();
+    int ncomp = 1;
+    if (saved0 > 1) {
+      for (int c = 1; c < 3 && c < static_cast<int>(ac.size()) && ncomp == 1; ++c) {
+        for (int i = 1; i < 256 && ncomp == 1; ++i)
+          if (dc0[c].counts[i] || ((i & 0xf) && ac[c].counts[i])) ncomp = 3;
+      }
+    }
+    JpegHistogram ach[3];
+    for (int c = 0; c < ncomp && c < static_cast<int>(ac.size()); ++c) ach[c] = ac[c];
+    size_t size = 0;
+    if (!cmp_->DeviceEncodeAndCompareKnown(img, jpg, params_.clear_metadata, dc0, ach, ncomp, &size))
+      return Fail(err);
+    pending_.clear();
+    pending_size_ = size;
+    has_pending_ = true;
+    pending_device_ = true;
+    res_->detail["encode_compare_s"] += Since(t0);
+    res_->detail["encode_known_histograms"] += 1;
+    return true;
+  }
   // Joins the pending encode and applies its MaybeOutput; returns its size.
   size_t FlushOutput() {
     if (!has_pending_) return 0;
@@ -1533,11 +1612,17 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   };
   std::vector<JpegHistogram> ac_histograms(ncomp);
   int jpg_header_size, dc_size;
+  // the components SaveToJpegData keeps at the start, and the DC histograms
+  // (the back end changes AC coefficients only: they stay as they are)
+  int saved0 = 3;
+  JpegHistogram dc0[3];
   {
     JpegHistogram dc_h[3], ac_h[3];
     int saved = cmp_->DeviceHistograms(*img, dc_h, ac_h);
     if (saved < 0 && cmp_->HasDeviceWriter()) return Fail(err);
     if (saved < 0) saved = CoeffImageHistograms(*img, scratch_.get(), dc_h, ac_h);
+    saved0 = saved;
+    for (int c = 0; c < 3; ++c) dc0[c] = dc_h[c];
     JpegData out;
     out.app_data = jpg.app_data;
     out.com_data = jpg.com_data;
@@ -1725,7 +1810,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           });
           JpegHistogram ac_now[3];
           if (!cmp_->DeviceBulkApply(*img, direction, bulk_cnt8.data(), ac_now)) return Fail(err);
-          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          for (int c = 0; c < ncomp && c < saved0 && c < 3; ++c) ac_histograms[c] = ac_now[c];
           img->host_partial = true;
           refresh_raw();
           loop.changed = static_cast<int>(bulk);
@@ -2042,7 +2127,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
-      if (!EncodeAndCompare(jpg, *img, err)) return false;
+      if (cmp_->HasKnownHistogramEncode() && !part_) {
+        // the candidate's histograms are the tracked ones: no histogram pass
+        if (!EncodeAndCompareKnown(jpg, *img, saved0, dc0, ac_histograms, err)) return false;
+      } else if (!EncodeAndCompare(jpg, *img, err)) {
+        return false;
+      }
       prev_size = est_jpg_size;
     }
   }

@@ -117,12 +117,23 @@ class Comparator {
     return false;
   }
   virtual bool DeviceOrderAdvance(float val_threshold, int direction) { return false; }
+  // DeviceEncodeAndCompare of a candidate whose symbol histograms the caller
+  // already has (the search back end tracks them exactly): the DC / AC
+  // histograms SaveToJpegData + WriteJpeg would count (comps at or above
+  // ncomp cleared), so the device only codes the scan -- no histogram pass,
+  // no wait for one.  HasKnownHistogramEncode() false: not supported.
+  virtual bool HasKnownHistogramEncode() const { return false; }
+  virtual bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                                           const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
+                                           size_t* size) {
+    return false;
+  }
   // The back end's bulk prefix on the device (with the device order only):
   // cnt[b] (< 256) changes of block b from the last_indexes of the last
   // DeviceChangeOrder, in `direction`, applied to the device copy of img
   // alone (the caller brings its host copy along lazily, host_partial), and
-  // the AC histograms of the changed image (as DeviceHistograms stores them)
-  // into ac.  HasDeviceBulk() false: apply it on the host.
+  // the AC histograms of the changed image into ac (every component's counts,
+  // none cleared).  HasDeviceBulk() false: apply it on the host.
   virtual bool HasDeviceBulk() const { return false; }
   virtual bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) {
     return false;
@@ -230,6 +241,10 @@ class HipButteraugliComparator : public Comparator {
                          std::vector<std::pair<int, float>>* order, int* blocks_to_change) override;
   bool DeviceOrderAdvance(float val_threshold, int direction) override;
   bool HasDeviceBulk() const override { return true; }
+  bool HasKnownHistogramEncode() const override { return true; }
+  bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                                   const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
+                                   size_t* size) override;
   bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   bool SetOriginalCoeffs420(const JpegData& jpg420) override;

@@ -146,6 +146,7 @@ class EngineCoder : public PartitionComparator::Coder {
   explicit EngineCoder(HipButteraugliComparator* hip) : hip_(hip), e_(hip->engine()) {}
   bool StageStart(const CoeffImage& img, int m0, int m1) override {
     if (!hip_->Sync(img) || !e_->JpegStageEnqueueRange(img.quant, m0, m1)) return Fail();
+    std::memcpy(quant_, img.quant, sizeof(quant_));  // (the scan's)
     return true;
   }
   bool StageWait(uint32_t* hist, uint64_t* chroma) override {
@@ -157,7 +158,7 @@ class EngineCoder : public PartitionComparator::Coder {
   }
   bool ScanStart(int ncomp, const JpegCodeTables& codes, int m0, int m1, uint64_t base,
                  bool pad_end) override {
-    return e_->JpegScanEnqueueRange(ncomp, codes, m0, m1, base, pad_end) || Fail();
+    return e_->JpegScanEnqueueRange(ncomp, quant_, codes, m0, m1, base, pad_end) || Fail();
   }
   bool Finish(std::vector<float>* block_max, PartitionComparator::Part* part) override {
     if (!e_->Sync()) return Fail();
@@ -190,6 +191,7 @@ class EngineCoder : public PartitionComparator::Coder {
   HipButteraugliComparator* hip_;
   Engine* e_;
   bool compare_ = false;
+  int quant_[3][64] = {};
 };
 
 // SaveToJpegData + EncodeScan (jpeg_data_writer.cc:447-538) of blocks

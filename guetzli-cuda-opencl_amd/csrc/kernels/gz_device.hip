@@ -444,8 +444,6 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_coeffs_), nc * sizeof(int16_t)) != hipSuccess)
     ok = false;
-  alloc(reinterpret_cast<void**>(&e->d_jzz_), nc * sizeof(int16_t));
-  alloc(reinterpret_cast<void**>(&e->d_jmask_), static_cast<size_t>(e->nb_) * 3 * 8);
   const size_t stage_groups = (3 * static_cast<size_t>(e->nb_) + kStageBlocks - 1) / kStageBlocks;
   alloc(reinterpret_cast<void**>(&e->d_jhist_), jhist_device_bytes(stage_groups));
   // worst case per MCU: 3 x (DC 16 + 11 bits, 63 x (16 + 10) bits, EOB 16) < 160 words
@@ -603,8 +601,8 @@ Engine::~Engine() {
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
-                  d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_, d_jzz_,
-                  d_jmask_, d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
+                  d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_,
+                  d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -1443,7 +1441,7 @@ bool Engine::JpegStageEnqueueRange(const int q[3][64], int m0, int m1) {
   // (the device counts are zero: cleared at creation, and by the last
   // workgroup of every stage after it has published them to h_jhist_)
   GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, kStageThreads, 0, s>>>(
-      d_cur_, qf, nb_, m0, m1, d_jzz_, d_jmask_, d_jhist_, m_jhist_));
+      d_cur_, qf, nb_, m0, m1, d_jhist_, m_jhist_));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;
 }
@@ -1457,20 +1455,19 @@ bool Engine::JpegStageWait(uint32_t* hist, uint64_t* chroma_nz) {
   return true;
 }
 
-bool Engine::JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff) {
-  // the pinned code staging may still feed the previous scan's copy
-  if (!Sync()) return false;
-  return JpegScanEnqueue(ncomp, codes) && Sync() && JpegScanFinish(nbits, ff);
+bool Engine::JpegScan(int ncomp, const int q[3][64], const JpegCodeTables& codes, uint64_t* nbits,
+                      uint64_t* ff) {
+  return JpegScanEnqueue(ncomp, q, codes) && Sync() && JpegScanFinish(nbits, ff);
 }
 
 // (the caller has synchronised since the previous scan: the pinned code
 // staging is free)
-bool Engine::JpegScanEnqueue(int ncomp, const JpegCodeTables& codes) {
-  return JpegScanEnqueueRange(ncomp, codes, 0, nb_, 0, true);
+bool Engine::JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes) {
+  return JpegScanEnqueueRange(ncomp, q, codes, 0, nb_, 0, true);
 }
 
-bool Engine::JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0, int m1, uint64_t base,
-                                  bool pad_end) {
+bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeTables& codes, int m0, int m1,
+                                  uint64_t base, bool pad_end) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
@@ -1501,7 +1498,10 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0
   uint64_t* status = reinterpret_cast<uint64_t*>(arr) + 1 + max_groups / 64 + 2;
   uint64_t* side = status + max_groups;
   uint32_t* seam = reinterpret_cast<uint32_t*>(side + 2 * max_groups);
-  GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_jzz_, nb_, m0, m1, ncomp, dc,
+  JpegQuantF qf;
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
+  GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
                                                             static_cast<unsigned long long>(base),
                                                             pad_end ? 1 : 0, words, ffc, arr, status, side,
                                                             seam, jepoch_, m_jhist_ + 6 * 256 + 2));

@@ -140,7 +140,7 @@ class Engine {
   // current one the kept one (the next scan overwrites the other);
   // JpegFetch copies a slot's bytes (MSB-first, valid until the next call).
   bool JpegStage(const int q[3][64], uint32_t* hist, uint64_t* chroma_nz);
-  bool JpegScan(int ncomp, const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff);
+  bool JpegScan(int ncomp, const int q[3][64], const JpegCodeTables& codes, uint64_t* nbits, uint64_t* ff);
   void JpegKeep() { jslot_ ^= 1; }
   bool JpegFetch(bool kept, const uint8_t** bytes, uint64_t* nbits);
   // The same steps split for overlap within one stream order: *Enqueue
@@ -152,7 +152,7 @@ class Engine {
   bool JpegStageEnqueue(const int q[3][64]);
   bool JpegStageWait(uint32_t* hist, uint64_t* chroma_nz);
   bool CompareEnqueue();
-  bool JpegScanEnqueue(int ncomp, const JpegCodeTables& codes);
+  bool JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes);
   bool Sync();
   void CompareFinish(float* distance, float* block_max);
   bool JpegScanFinish(uint64_t* nbits, uint64_t* ff);
@@ -171,8 +171,8 @@ class Engine {
     bool first_shared = false, last_open = false;
   };
   bool JpegStageEnqueueRange(const int q[3][64], int m0, int m1);
-  bool JpegScanEnqueueRange(int ncomp, const JpegCodeTables& codes, int m0, int m1, uint64_t base,
-                            bool pad_end);
+  bool JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeTables& codes, int m0, int m1,
+                            uint64_t base, bool pad_end);
   bool JpegScanFinishPart(ScanPart* part);
   // The stored words of a slot's part (memory byte order; words[0] is the
   // stream's word base >> 5, the shared ones zero) and its ScanPart.
@@ -277,8 +277,6 @@ class Engine {
   uint8_t* d_cand_idx_ = nullptr;  // [blocks * 192] compacted candidates
   float* d_cand_err_ = nullptr;
   int16_t* h_coeffs_ = nullptr;    // pinned [3][blocks][64] staging
-  int16_t* d_jzz_ = nullptr;       // device entropy coder: quantized zigzag
-  uint64_t* d_jmask_ = nullptr;    //   non-zero masks [3][blocks]
   uint32_t* d_jhist_ = nullptr;    //   kJHistCopies x 6 x 256 counts + chroma non-zeros (u64) + done counter
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
