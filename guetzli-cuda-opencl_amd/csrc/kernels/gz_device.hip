@@ -1475,7 +1475,8 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   JpegCodesArg dc;
   for (int c = 0; c < 3; ++c) {
     for (int i = 0; i < 256; ++i) {
-      if (i >= kJDcSyms && codes.dc_len[c][i]) return Fail("JpegScan DC category above 16", 0);
+      if (i >= kJDcSyms && codes.dc_len[c][i] >= 1 && codes.dc_len[c][i] <= 16)
+        return Fail("JpegScan DC category above 16", 0);
       if (i < kJDcSyms) {
         dc.dc[c][i][0] = static_cast<uint8_t>(codes.dc_code[c][i]);
         dc.dc[c][i][1] = static_cast<uint8_t>(codes.dc_code[c][i] >> 8);
