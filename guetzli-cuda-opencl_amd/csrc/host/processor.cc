@@ -606,17 +606,14 @@ bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direct
                                                JpegHistogram ac[3]) {
   const auto t0 = Clock::now();
   if (!SyncCoeffs(img)) return false;
-  uint32_t hist[6 * 256];
-  uint64_t chroma = 0;
-  if (!engine_->BulkApply(direction, img.quant, cnt, hist, &chroma)) {
+  int32_t delta[3][256];
+  if (!engine_->BulkApply(direction, img.quant, cnt, delta)) {
     err_ = engine_->error();
     return false;
   }
-  for (int c = 0; c < 3; ++c) {  // (every component: the back end's convention)
-    ac[c].Clear();
-    for (int i = 0; i < 256; ++i) ac[c].counts[i] = 2 * hist[(2 * c + 1) * 256 + i];
-  }
-  (void)chroma;
+  // (the counts are stored doubled, JpegHistogram::Add)
+  for (int c = 0; c < 3; ++c)
+    for (int i = 0; i < 256; ++i) ac[c].counts[i] += 2u * static_cast<uint32_t>(delta[c][i]);
   seconds_bulk += Since(t0);
   return true;
 }
@@ -1662,8 +1659,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   bool device_order = false;
   if (!part_ && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
   // With the device order the bulk prefix is applied on the device too
-  // (DeviceBulkApply), with the AC histograms recounted there.  The host copy
-  // of a block then follows lazily: a block's coefficients are a function of
+  // (DeviceBulkApply), with the change of the AC histograms counted there.
+  // The host copy of a block then follows lazily: a block's coefficients are a function of
   // its last_indexes alone -- its first last_indexes[b] candidates zeroed,
   // the others as quantized (up iterations zero candidates in order, down
   // iterations restore them in reverse) -- so mat_li[b], the last_indexes the
@@ -1809,8 +1806,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           });
           JpegHistogram ac_now[3];
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_now[c] = ac_histograms[c];
           if (!cmp_->DeviceBulkApply(*img, direction, bulk_cnt8.data(), ac_now)) return Fail(err);
-          for (int c = 0; c < ncomp && c < saved0 && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
           img->host_partial = true;
           refresh_raw();
           loop.changed = static_cast<int>(bulk);

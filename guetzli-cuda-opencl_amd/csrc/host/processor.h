@@ -131,9 +131,10 @@ class Comparator {
   // The back end's bulk prefix on the device (with the device order only):
   // cnt[b] (< 256) changes of block b from the last_indexes of the last
   // DeviceChangeOrder, in `direction`, applied to the device copy of img
-  // alone (the caller brings its host copy along lazily, host_partial), and
-  // the AC histograms of the changed image into ac (every component's counts,
-  // none cleared).  HasDeviceBulk() false: apply it on the host.
+  // alone (the caller brings its host copy along lazily, host_partial); ac
+  // holds every component's AC histograms before the changes on entry and
+  // after them on return (the same counts as the host's per-change updates).
+  // HasDeviceBulk() false: apply it on the host.
   virtual bool HasDeviceBulk() const { return false; }
   virtual bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) {
     return false;

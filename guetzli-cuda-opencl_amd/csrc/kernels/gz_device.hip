@@ -596,6 +596,17 @@ static hipError_t WaitOnStream(hipStream_t s) {
   return hipSuccess;
 }
 
+// A wait for work of unknown length (a copy or kernels that may sit behind
+// other streams' work on a shared device): none if the stream is already
+// idle, else the sleeping wait (the runtime's synchronisation polls a core
+// for as long as it waits).
+static hipError_t WaitIdle(hipStream_t s) {
+  const hipError_t q = hipStreamQuery(s);
+  if (q == hipSuccess) return hipSuccess;
+  if (q != hipErrorNotReady) return q;
+  return WaitOnStream(s);
+}
+
 Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
@@ -634,7 +645,7 @@ bool Engine::SetReference(const uint8_t* rgb, bool device_ptr) {
     GZ_TIMED("ref_opsin", k_opsin2d<<<tx * ty, 256, 0, s>>>(d_lin_, w_, h_, tx, d_ref_xyb_, d_scales_,
                                                               scale_stride_));
   }
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitIdle(s));
   ProfFlush();
   have_mask_scale_ = false;
   return true;
@@ -645,7 +656,7 @@ bool Engine::SetOriginalCoeffs(const int16_t* coeffs, bool device_ptr) {
   GZ_HIP(hipSetDevice(device_));
   GZ_HIP(hipMemcpyAsync(d_orig_, coeffs, static_cast<size_t>(nb_) * 64 * 3 * sizeof(int16_t),
                         device_ptr ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitIdle(s));
   ProfFlush();
   return true;
 }
@@ -656,7 +667,7 @@ bool Engine::ComputeOriginalCoeffs(int16_t* host_out) {
   const size_t nc = static_cast<size_t>(nb_) * 64 * 3;
   GZ_TIMED("rgb_to_coeffs", k_rgb_to_coeffs<<<(3 * nb_ + 63) / 64, 64, 0, s>>>(d_rgb_, w_, h_, bw_, nb_, d_orig_));
   GZ_HIP(hipMemcpyAsync(h_coeffs_, d_orig_, nc * sizeof(int16_t), hipMemcpyDeviceToHost, s));
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitIdle(s));
   ProfFlush();
   memcpy(host_out, h_coeffs_, nc * sizeof(int16_t));
   return true;
@@ -686,7 +697,7 @@ bool Engine::UploadCoeffDelta(const uint32_t* idx, const int16_t* val, size_t n)
   cand_src_ = kCandCoeffs;
   if (n == 0) return true;
   // the previous delta's kernel may still read the pinned staging
-  GZ_HIP(hipStreamSynchronize(s));
+  GZ_HIP(WaitIdle(s));
   if (n > delta_cap_) {
     if (h_delta_idx_) GZ_HIP(hipHostFree(h_delta_idx_));
     if (h_delta_val_) GZ_HIP(hipHostFree(h_delta_val_));
@@ -718,7 +729,7 @@ bool Engine::QuantizeFromOriginal(const int q[3][64], int16_t* host_out) {
   GZ_TIMED("quantize", k_quantize<<<dim3((per + 255) / 256, 3), 256, 0, s>>>(d_orig_, qm, per, d_cur_));
   if (host_out) {  // through the pinned staging: a DMA, no pageable bounce
     GZ_HIP(hipMemcpyAsync(h_coeffs_, d_cur_, 3 * per * sizeof(int16_t), hipMemcpyDeviceToHost, s));
-    GZ_HIP(hipStreamSynchronize(s));
+    GZ_HIP(WaitIdle(s));
     memcpy(host_out, h_coeffs_, 3 * per * sizeof(int16_t));
   }
   ProfFlush();
@@ -903,7 +914,6 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
 }
 
 bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
-  hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (dbg) {
     if (!EnqueueCompare(dbg)) return false;
@@ -1174,7 +1184,7 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
   if (total) {
     GZ_HIP(hipMemcpyAsync(h_cand_idx_, d_cand_idx_, total, hipMemcpyDeviceToHost, s));
     GZ_HIP(hipMemcpyAsync(h_cand_err_, d_cand_err_, total * 4, hipMemcpyDeviceToHost, s));
-    GZ_HIP(hipStreamSynchronize(s));
+    GZ_HIP(WaitIdle(s));
   }
   ProfFlush();
   offsets->assign(h_zero_off_, h_zero_off_ + nblocks + 1);
@@ -1308,8 +1318,7 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   return true;
 }
 
-bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, uint32_t* hist,
-                       uint64_t* chroma_nz) {
+bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("BulkApply without a change order", 0);
@@ -1333,15 +1342,21 @@ bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt
   const OrdLayout L(nb_);
   QuantMatrix qm;
   memcpy(qm.q, quant, sizeof(qm.q));
-  GZ_TIMED("bulk_apply", k_bulk_apply<<<static_cast<unsigned>((nb_ + 255) / 256), 256, 0, s>>>(
+  JpegQuantF qf;
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(quant[c][c_natural_order[k]]);
+  // (at most as many workgroups as the histogram stage has arrival counters)
+  const size_t stage_groups = (3 * static_cast<size_t>(nb_) + kStageBlocks - 1) / kStageBlocks;
+  const unsigned groups = static_cast<unsigned>(
+      std::min(stage_groups, (static_cast<size_t>(nb_) + kBulkWaves - 1) / kBulkWaves));
+  GZ_TIMED("bulk_apply", k_bulk_apply<<<groups, kBulkThreads, 0, s>>>(
       m_bulk_, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
-      d_cand_idx_, nb_, direction, d_orig_, qm, d_cur_));
-  if (!JpegStageEnqueue(quant)) return false;
+      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_));
   // (a sleeping wait: nothing else of this frame is queued behind it)
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
-  memcpy(hist, h_jhist_, 6 * 256 * 4);
-  memcpy(chroma_nz, h_jhist_ + 6 * 256, 8);
+  for (int c = 0; c < 3; ++c)
+    for (int i = 0; i < 256; ++i) delta[c][i] = static_cast<int32_t>(h_jhist_[(2 * c + 1) * 256 + i]);
   return true;
 }
 
@@ -1475,6 +1490,7 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   JpegCodesArg dc;
   for (int c = 0; c < 3; ++c) {
     for (int i = 0; i < 256; ++i) {
+      // (an absent symbol's length is 0 or 255: HuffCodeTable's fill)
       if (i >= kJDcSyms && codes.dc_len[c][i] >= 1 && codes.dc_len[c][i] <= 16)
         return Fail("JpegScan DC category above 16", 0);
       if (i < kJDcSyms) {

@@ -199,11 +199,10 @@ class Engine {
   bool OrderAdvance(float val_threshold, int direction);
   // The back end's bulk prefix applied to the device copy (k_bulk_apply):
   // cnt[b] changes of block b from the last_indexes of this iteration's
-  // OrderBuild, zeroed (direction 1) or restored to Quantize(orig, quant);
-  // then the histogram stage of the changed image (as JpegStage: hist,
-  // chroma_nz), waited for.
-  bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, uint32_t* hist,
-                 uint64_t* chroma_nz);
+  // OrderBuild, zeroed (direction 1) or restored to Quantize(orig, quant),
+  // and the change of every component's AC symbol counts it makes
+  // (delta[c][symbol], unscaled), waited for.
+  bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]);
 
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }

@@ -55,6 +55,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     import torch
     import guetzli_amd as gz
+    # the ranks' host work runs on the library's pool; torch's intra-op
+    # threads (the gathered blocks' copies) would spin after each collective
+    # on every rank at once
+    torch.set_num_threads(1)
     dist = None
     if args.one_device:
         local = 0
@@ -87,8 +91,14 @@ def main():
     cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     th1 = _thread_cpu()
     threads = {}
+    import threading
+    main_tid = str(threading.get_native_id())
+    per_tid = []
     for k, (c, n) in th1.items():
-        threads[n] = threads.get(n, 0.0) + c - th0.get(k, (0.0, n))[0]
+        d = c - th0.get(k, (0.0, n))[0]
+        threads[n] = threads.get(n, 0.0) + d
+        per_tid.append((d, ("main:" if k == main_tid else "") + n))
+    per_tid.sort(reverse=True)
     detail = gz.last_process_detail()
     host_cpu = [cpu]
     if dist is not None:
@@ -114,6 +124,7 @@ def main():
            "host_cpu_seconds_per_rank": [round(x, 3) for x in host_cpu],
            "rank0_thread_cpu_seconds": {n: round(c, 3) for n, c in
                                         sorted(threads.items(), key=lambda x: -x[1]) if c > 0.01},
+           "rank0_top_threads": [[n, round(c, 3)] for c, n in per_tid[:8]],
            "detail": detail}
     if args.check and rank == 0:
         # the single-engine path on this rank's GPU (the others wait)
