@@ -14,6 +14,7 @@ for lib in "$@"; do
   i=$((i + 1))
   if [ "$lib" = default ]; then unset GZ_LIB_PATH; else export GZ_LIB_PATH=$PWD/$lib; fi
   echo "== $i: $lib"
+  if [ -z "$GZ_AB_NO_PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof$i -o run --output-format csv \
     -- python $BENCH > $O/${i}_prof.json 2> $O/${i}_prof.err || { tail $O/${i}_prof.err; exit 1; }
   python - $O/prof$i/run_kernel_stats.csv <<'PY'
@@ -24,8 +25,15 @@ for r in rows[:12]:
     print("  %-40s calls %6s avg %8.1f us  %5.1f%%" % (r["Name"].split("(")[0][-40:], r["Calls"],
           float(r["AverageNs"]) / 1e3, float(r["Percentage"])))
 PY
+  fi
   for r in 1 2; do
     timeout -k 10 200 python $BENCH > $O/${i}_bench$r.json 2> $O/${i}_bench$r.err || { tail $O/${i}_bench$r.err; exit 1; }
-    python -c "import json; d=json.loads(open('$O/${i}_bench$r.json').read().strip().splitlines()[-1]); print('bench', d['value'], d['ms_per_step'], d['host_cpu_seconds_per_frame'], d['verified']['bit_exact'])"
+    # throughput, host CPU per frame, and the isolated frame's per-region ms
+    python -c "
+import json
+d = json.loads(open('$O/${i}_bench$r.json').read().strip().splitlines()[-1])
+g = d.get('gpu_regions_ms_per_frame', {})
+print('bench', d['value'], d['ms_per_step'], d['host_cpu_seconds_per_frame'], d['verified']['bit_exact'],
+      {k: g.get(k) for k in '${GZ_AB_REGIONS:-jpeg_code jpeg_stage bulk_apply block_zeroing}'.split()})"
   done
 done

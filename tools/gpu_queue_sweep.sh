@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/queues
 mkdir -p $O
-ARGS="--no-cpu-baseline --no-large-frame --steps ${GZ_STEPS:-4} --warmup 1"
+ARGS="--no-cpu-baseline --no-large-frame --no-uhd-frame --steps ${GZ_STEPS:-4} --warmup 1"
 for r in $(seq ${GZ_ROUNDS:-1}); do
 for n in ${GZ_INFLIGHT:-10}; do
   for cfg in ${GZ_CONFIGS:-4:hostfunc 8:event 4:event}; do
