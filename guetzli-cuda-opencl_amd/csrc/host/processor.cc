@@ -12,6 +12,7 @@
 #include "host/processor.h"
 
 #include <algorithm>
+#include <limits>
 #include <time.h>
 
 #include <chrono>
@@ -184,13 +185,27 @@ bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
   return true;
 }
 
+const std::vector<float>& HipButteraugliComparator::block_max_distance() const {
+  if (block_max_stale_) {
+    float d = 0.0f;
+    if (engine_->CompareFinish(&d, block_max_.data())) {
+      block_max_stale_ = false;
+    } else {
+      err_ = engine_->error();
+      std::fill(block_max_.begin(), block_max_.end(), std::numeric_limits<float>::infinity());
+    }
+  }
+  return block_max_;
+}
+
 bool HipButteraugliComparator::Compare(const CoeffImage& img) {
   const auto t0 = Clock::now();
   if (!SyncCoeffs(img)) return false;
-  if (!engine_->Compare(&distance_, block_max_.data(), nullptr)) {
+  if (!engine_->Compare(&distance_, nullptr, nullptr)) {
     err_ = engine_->error();
     return false;
   }
+  block_max_stale_ = true;
   ++compares;
   seconds_compare += Since(t0);
   return true;
@@ -383,7 +398,8 @@ bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const
       err_ = e->error();
       return false;
     }
-    e->CompareFinish(&distance_, block_max_.data());
+    (void)e->CompareFinish(&distance_, nullptr);
+    block_max_stale_ = true;
     ++compares;
     seconds_compare += Since(t0);
     cpu_compare += ThreadCpu() - c0;
@@ -410,7 +426,8 @@ bool HipButteraugliComparator::EncodeAndCompareWith(const CoeffImage& img, const
   }
   seconds_wait += Since(tw1);
   cpu_wait += ThreadCpu() - cw1;
-  e->CompareFinish(&distance_, block_max_.data());
+  (void)e->CompareFinish(&distance_, nullptr);
+  block_max_stale_ = true;
   ++compares;
   // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
@@ -540,10 +557,11 @@ bool HipButteraugliComparator::Compare420(const Image420& img) {
   device_ = CoeffCursor();
   if (!engine_->Set420(img.y.data(), img.c[0].data(), img.c[1].data(), img.plane[0].px.data(),
                        img.plane[1].px.data()) ||
-      !engine_->Compare(&distance_, block_max_.data(), nullptr)) {
+      !engine_->Compare(&distance_, nullptr, nullptr)) {
     err_ = engine_->error();
     return false;
   }
+  block_max_stale_ = true;
   ++compares;
   seconds_compare += Since(t0);
   return true;
@@ -656,7 +674,8 @@ bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img
   }
   seconds_wait += Since(tw);
   cpu_wait += ThreadCpu() - cw;
-  e->CompareFinish(&distance_, block_max_.data());
+  (void)e->CompareFinish(&distance_, nullptr);
+  block_max_stale_ = true;
   ++compares;
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
   *size = cur_size_;

@@ -230,7 +230,9 @@ class HipButteraugliComparator : public Comparator {
   double ScoreOutputSize(int size) const override;
   bool DistanceOK(double target_mul) const override { return distance_ <= target_mul * target_; }
   float distmap_aggregate() const override { return distance_; }
-  const std::vector<float>& block_max_distance() const override { return block_max_; }
+  // (copied from the device on first use after a Compare: the device change
+  // order reads them in HBM, so the search itself never asks)
+  const std::vector<float>& block_max_distance() const override;
   float BlockErrorLimit() const override { return target_; }
   void ComputeBlockErrorAdjustmentWeights(int direction, int max_block_dist, double target_mul,
                                           int factor_x, int factor_y,
@@ -291,12 +293,13 @@ class HipButteraugliComparator : public Comparator {
   int w_ = 0, h_ = 0;
   float target_ = 0.0f;
   float distance_ = 0.0f;
-  std::vector<float> block_max_;
+  mutable std::vector<float> block_max_;
+  mutable bool block_max_stale_ = false;  // the last Compare's maxima are on the device only
   CoeffCursor device_;  // what the device copy of the coefficients reflects
   bool IsOriginal(const CoeffImage& img) const;
   std::string cur_prologue_, kept_prologue_;  // headers of the encoded / kept candidates
   size_t cur_size_ = 0, kept_size_ = 0;
-  std::string err_;
+  mutable std::string err_;
 };
 
 struct ProcessParams {  // guetzli::Params, processor.h:34-42

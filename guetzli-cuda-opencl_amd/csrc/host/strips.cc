@@ -165,7 +165,7 @@ class EngineCoder : public PartitionComparator::Coder {
     if (compare_) {
       float d = 0.0f;
       block_max->resize(e_->blocks());
-      e_->CompareFinish(&d, block_max->data());
+      if (!e_->CompareFinish(&d, block_max->data())) return Fail();
       compare_ = false;
     }
     if (part) {

@@ -469,6 +469,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_block_max_), e->h_block_max_, 0) != hipSuccess)
     ok = false;
+  alloc(reinterpret_cast<void**>(&e->d_dmax_), 64);  // k_distance's word + arrival counters
+  if (ok && hipMemsetAsync(e->d_dmax_, 0, 64, s) != hipSuccess) ok = false;
+
   if (!ok) return fail("device allocation failed");
   // pinned staging (coefficients, offsets, histograms, block maxima)
   e->bytes_ += nc * sizeof(int16_t) + static_cast<size_t>(e->nb_) * 12 + 8192;
@@ -614,7 +617,7 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_,
                   d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_};
+                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (void* g : compare_graph_)
@@ -906,7 +909,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
-                                                              dm, d_block_max_, m_block_max_));
+                                                              dm, d_block_max_));
+    GZ_TIMED("distance", k_distance<<<kDistGroups, 256, 0, s>>>(d_block_max_, nb_, d_dmax_, m_block_max_ + nb_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");
@@ -921,8 +925,7 @@ bool Engine::Compare(float* distance, float* block_max, CompareDebug* dbg) {
     return false;
   }
   if (!Sync()) return false;
-  CompareFinish(distance, block_max);
-  return true;
+  return CompareFinish(distance, block_max);
 }
 
 bool Engine::CompareEnqueue() {
@@ -950,7 +953,7 @@ bool Engine::CompareEnqueue() {
     }
     GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graph), s));
   }
-  // (the block maxima reach h_block_max_ from k_diffmap_final itself)
+  // (the distance reaches h_block_max_[nb_] from k_diffmap_final itself)
   return true;
 }
 
@@ -960,11 +963,16 @@ bool Engine::Sync() {
   return true;
 }
 
-void Engine::CompareFinish(float* distance, float* block_max) {
-  float d = 0.0f;
-  for (int b = 0; b < nb_; ++b) d = d < h_block_max_[b] ? h_block_max_[b] : d;
-  if (block_max) memcpy(block_max, h_block_max_, nb_ * 4);
-  *distance = d;
+bool Engine::CompareFinish(float* distance, float* block_max) {
+  *distance = h_block_max_[nb_];
+  if (block_max) {
+    hipStream_t s = static_cast<hipStream_t>(stream_);
+    GZ_HIP(hipSetDevice(device_));
+    GZ_HIP(hipMemcpyAsync(h_block_max_, d_block_max_, static_cast<size_t>(nb_) * 4, hipMemcpyDeviceToHost, s));
+    GZ_HIP(WaitIdle(s));
+    memcpy(block_max, h_block_max_, static_cast<size_t>(nb_) * 4);
+  }
+  return true;
 }
 
 bool Engine::StartBlockComparisons(float* mask_scale_host) {
@@ -1094,12 +1102,12 @@ static size_t BzLdsPad() {
 }
 
 // offsets[0..n] = exclusive prefix sums of the device counts[0..n), on the stream.
-bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name) {
+bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (n > nb_) return Fail("ScanCounts size", 0);
   const unsigned chunks = static_cast<unsigned>((n + kScanChunk - 1) / kScanChunk);
   GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
-                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets)));
+                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets, first)));
   return true;
 }
 
@@ -1195,12 +1203,12 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 
 // ---- the back end's change order (order_kernels.inc) ----
 // Host <-> device traffic through mapped pinned memory (no copy launches):
-// the kernels read last_indexes from h_ord_ and write the totals after it
+// the kernels read last_indexes (bytes) from h_ord_ and write the totals after it
 // and the entries into h_ord_entries_; the host reads them after the
 // stream synchronisation.
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, info, arr, mbe, last, bytes;
+  size_t weight, active, cnt, off, info, arr, mbe, last, first, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
@@ -1211,7 +1219,8 @@ struct OrdLayout {
     arr = info + 256;                               // arrival counters: 1 + groups / 64 + 1
     mbe = arr + ((n / 256 / 64 + 2) * 4 + 255) / 256 * 256;
     last = mbe + a;
-    bytes = last + a;
+    first = last + a;  // the fill's tile starts: (entries <= 193 n) / 256 + 1 <= n + 4
+    bytes = first + ((n + 4) * 4 + 255) / 256 * 256;
   }
 };
 }  // namespace
@@ -1257,7 +1266,7 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   char* base = static_cast<char*>(d_ord_);
   float* weight = reinterpret_cast<float*>(base + L.weight);
   int* active = reinterpret_cast<int*>(base + L.active);
-  const OrderArgs a{reinterpret_cast<int*>(base + L.last), m_ord_, d_zero_off_, ord_cand_n_, direction,
+  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, direction,
                     reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.info),
                     reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
   const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
@@ -1267,7 +1276,15 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
     // them to the device and applies the previous iteration's
     // max_block_error update (the previous build's kernels, which read the
     // staging, have completed: the host synchronised on them)
-    memcpy(h_ord_, last_indexes.data(), static_cast<size_t>(nb_) * 4);
+    // (as bytes: a block has at most 3 x 63 candidates; the kernel reads
+    // them across PCIe, a quarter of the int array's bytes)
+    uint8_t* l8 = reinterpret_cast<uint8_t*>(h_ord_);
+    int bad = 0;
+    for (int b = 0; b < nb_; ++b) {
+      bad |= last_indexes[b] & ~0xff;
+      l8[b] = static_cast<uint8_t>(last_indexes[b]);
+    }
+    if (bad) return Fail("OrderBuild: last index above 255", 0);
     adv_dir = ord_adv_dir_;
     ord_adv_dir_ = 0;
   }
@@ -1305,13 +1322,14 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   char* base = static_cast<char*>(d_ord_);
   int* cnt = reinterpret_cast<int*>(base + L.cnt);
   int* off = reinterpret_cast<int*>(base + L.off);
-  const OrderArgs a{reinterpret_cast<int*>(base + L.last), m_ord_, d_zero_off_, ord_cand_n_, ord_direction_, cnt,
+  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, ord_direction_, cnt,
                     reinterpret_cast<int*>(base + L.info), reinterpret_cast<uint32_t*>(base + L.arr),
                     m_ord_ + nb_};
-  if (!ScanCounts(cnt, nb_, off, "order_scan")) return false;
+  int* first = reinterpret_cast<int*>(base + L.first);
+  if (!ScanCounts(cnt, nb_, off, "order_scan", first)) return false;
   GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(
       reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
-      off, static_cast<int>(n), static_cast<OrderEntry*>(m_ord_entries_), a));
+      off, static_cast<int>(n), first, static_cast<OrderEntry*>(m_ord_entries_), a));
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
   memcpy(static_cast<void*>(out), h_ord_entries_, bytes);

@@ -154,7 +154,9 @@ class Engine {
   bool CompareEnqueue();
   bool JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes);
   bool Sync();
-  void CompareFinish(float* distance, float* block_max);
+  // distance: the pass's maximum (from mapped memory); block_max (may be
+  // null): the per-block maxima, copied from HBM.
+  bool CompareFinish(float* distance, float* block_max);
   bool JpegScanFinish(uint64_t* nbits, uint64_t* ff);
 
   // The coder over a part of the scan (a frame split over ranks by block
@@ -177,8 +179,9 @@ class Engine {
   // The stored words of a slot's part (memory byte order; words[0] is the
   // stream's word base >> 5, the shared ones zero) and its ScanPart.
   bool JpegFetchPart(bool kept, std::vector<uint32_t>* words, ScanPart* part);
-  // offsets[i] = counts[0] + ... + counts[i - 1] on the device (n + 1 entries)
-  bool ScanCounts(const int* counts, int n, int* offsets, const char* name);
+  // offsets[i] = counts[0] + ... + counts[i - 1] on the device (n + 1
+  // entries); first (optional): the index holding element 256 c, per c
+  bool ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first = nullptr);
   bool OrderBlocks(int comp_mask);
 
   // The search back end's change order on the device (SelectFrequencyBackEnd,
@@ -302,8 +305,9 @@ class Engine {
   size_t cbreq_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
-  float* h_block_max_ = nullptr;   // mapped: k_diffmap_final writes the block maxima here too
+  float* h_block_max_ = nullptr;   // pinned: the block maxima on request; [nb_]: the distance (mapped)
   float* m_block_max_ = nullptr;
+  uint32_t* d_dmax_ = nullptr;      // k_distance's maximum word + arrival counters
   // device change order (allocated on first use): weight f32 | active i32 |
   // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
   // max_block_error f32 | last_indexes i32
