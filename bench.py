@@ -90,6 +90,7 @@ def stage_bytes_per_px():
     s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
     s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
     s["diffmap_final"] = 4 / 9.0 + 4 / 4.0 + 4 / 64.0
+    s["distance"] = 4 / 64.0                          # the block maxima, read once
     return s
 
 
@@ -105,15 +106,15 @@ ZEROING_BYTES_PER_KEPT = 1 + 4
 # The launches of one search-loop Compare pass (each kernel once; the other
 # entries above are the stage-dump path's or their fused parts).
 PASS_KERNELS = ("coeffs_to_linear", "opsin_mhic", "edge_mask", "block_diff", "blur_h", "blur_v",
-                "combine_channels", "diffmap_blur_h", "diffmap_blur_v", "diffmap_final")
+                "combine_channels", "diffmap_blur_h", "diffmap_blur_v", "diffmap_final", "distance")
 
 
 # The device entropy coder, per MCU (4:4:4: one 8x8 block per component):
-# k_jpeg_stage reads the 3 x 64 int16 coefficients and writes their 3 x 64
-# int16 quantized zigzag copies and 3 non-zero masks (u64); k_jpeg_code reads
-# the zigzag coefficients (the scan it writes, ~2-5 % of that at q95, is not
-# counted; its per-workgroup code table copies are L2 traffic).
-JPEG_STAGE_BYTES_PER_MCU = 3 * 64 * 2 * 2 + 3 * 8
+# k_jpeg_stage reads the 3 x 64 int16 stored coefficients (its histograms
+# are a few KB per launch); k_jpeg_code reads them again and quantizes in
+# place (the scan it writes, ~2-5 % of that at q95, is not counted; the code
+# tables arrive as kernel arguments).
+JPEG_STAGE_BYTES_PER_MCU = 3 * 64 * 2
 JPEG_CODE_BYTES_PER_MCU = 3 * 64 * 2
 
 
@@ -156,12 +157,13 @@ STAGE_SYMBOL = {
     "block_zeroing": "gz::k_block_zeroing(", "jpeg_stage": "gz::k_jpeg_stage(",
     "jpeg_code": "gz::k_jpeg_code(",
     "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
+    "distance": "gz::k_distance(",
 }
 
 
 def measured_traffic(stage, w, h):
     """HBM bytes per launch of `stage` from the committed rocprofv3 PMC
-    summary (tools/gpu_profile.sh -> profiles/*traffic*.json: FETCH_SIZE x2
+    summary (tools/gpu_round.sh -> profiles/*traffic*.json: FETCH_SIZE x2
     + WRITE_SIZE, same frame size), or None."""
     import glob
     sym = STAGE_SYMBOL.get(stage)
