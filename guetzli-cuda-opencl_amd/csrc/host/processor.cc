@@ -604,18 +604,12 @@ bool HipButteraugliComparator::DeviceChangeOrder(int direction, double target_mu
   const double td = target_ * target_mul;
   for (int rblock = 1; rblock <= 4; ++rblock) {
     size_t n = 0;
-    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, &n, blocks_to_change)) {
+    // (the entries come back with the counts: one wait per radius)
+    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, &n, blocks_to_change, order)) {
       err_ = engine_->error();
       return false;
     }
-    order->resize(n);
-    if (n) {
-      if (!engine_->OrderFetch(order->data(), n)) {
-        err_ = engine_->error();
-        return false;
-      }
-      break;
-    }
+    if (n) break;
   }
   return true;
 }

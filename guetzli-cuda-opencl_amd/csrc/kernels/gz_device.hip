@@ -1256,10 +1256,15 @@ bool Engine::OrderReset() {
 }
 
 bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
-                        const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change) {
+                        const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change,
+                        std::vector<std::pair<int, float>>* entries) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderBuild without candidates", 0);
+  // (the fused fill writes at most cand_n + nb entries: the mapped buffer
+  // holds that many before anything is queued)
+  const size_t max_entries = static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_);
+  if (entries && !OrderEntriesCapacity(max_entries)) return false;
   if (static_cast<int>(last_indexes.size()) != nb_ || rblock < 1 || rblock > 4)
     return Fail("OrderBuild arguments", 0);
   const OrdLayout L(nb_);
@@ -1293,11 +1298,54 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
                                                                 reinterpret_cast<float*>(base + L.mbe),
                                                                 ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, a));
   if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
+  ord_direction_ = direction;
+  // with `entries`: the offsets and the entries queued behind the counts
+  // (the fill reads the total from the offsets; a grid for the largest
+  // possible count, its workgroups past the total leave at once), one wait
+  if (entries && !OrderFillEnqueue(max_entries)) return false;
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
   *blocks_to_change = h_ord_[nb_ + rblock - 1];
   *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
-  ord_direction_ = direction;
+  if (entries) {
+    entries->resize(*n_entries);
+    if (*n_entries)
+      memcpy(static_cast<void*>(entries->data()), h_ord_entries_, *n_entries * sizeof(OrderEntry));
+  }
+  return true;
+}
+
+bool Engine::OrderEntriesCapacity(size_t n) {
+  const size_t bytes = n * sizeof(OrderEntry);
+  if (bytes > h_ord_entries_cap_) {
+    if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
+    h_ord_entries_ = nullptr;
+    h_ord_entries_cap_ = 0;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap, hipHostMallocCoherent));
+    GZ_HIP(hipHostGetDevicePointer(&m_ord_entries_, h_ord_entries_, 0));
+    h_ord_entries_cap_ = cap;
+  }
+  return true;
+}
+
+// the scan of this build's counts and the fill of up to `grid_entries`
+// entries (the fill takes the true total from the scan)
+bool Engine::OrderFillEnqueue(size_t grid_entries) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  int* cnt = reinterpret_cast<int*>(base + L.cnt);
+  int* off = reinterpret_cast<int*>(base + L.off);
+  int* first = reinterpret_cast<int*>(base + L.first);
+  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_,
+                    ord_cand_n_, ord_direction_, cnt, reinterpret_cast<int*>(base + L.info),
+                    reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
+  if (!ScanCounts(cnt, nb_, off, "order_scan", first)) return false;
+  if (grid_entries == 0) return true;
+  GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((grid_entries + 255) / 256), 256, 0, s>>>(
+      reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
+      off, first, static_cast<OrderEntry*>(m_ord_entries_), a));
   return true;
 }
 
@@ -1309,30 +1357,10 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   // (at most cand_n + nb: a block past the last candidate reads one, the
   // host's clamp of its offset into [0, cand_n - 1])
   if (n > static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_)) return Fail("OrderFetch entry count", 0);
-  const size_t bytes = n * sizeof(OrderEntry);
-  if (bytes > h_ord_entries_cap_) {
-    if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
-    h_ord_entries_ = nullptr;
-    const size_t cap = bytes + bytes / 4 + 4096;
-    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap, hipHostMallocCoherent));
-    GZ_HIP(hipHostGetDevicePointer(&m_ord_entries_, h_ord_entries_, 0));
-    h_ord_entries_cap_ = cap;
-  }
-  const OrdLayout L(nb_);
-  char* base = static_cast<char*>(d_ord_);
-  int* cnt = reinterpret_cast<int*>(base + L.cnt);
-  int* off = reinterpret_cast<int*>(base + L.off);
-  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, ord_direction_, cnt,
-                    reinterpret_cast<int*>(base + L.info), reinterpret_cast<uint32_t*>(base + L.arr),
-                    m_ord_ + nb_};
-  int* first = reinterpret_cast<int*>(base + L.first);
-  if (!ScanCounts(cnt, nb_, off, "order_scan", first)) return false;
-  GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(
-      reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
-      off, static_cast<int>(n), first, static_cast<OrderEntry*>(m_ord_entries_), a));
+  if (!OrderEntriesCapacity(n) || !OrderFillEnqueue(n)) return false;
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
-  memcpy(static_cast<void*>(out), h_ord_entries_, bytes);
+  memcpy(static_cast<void*>(out), h_ord_entries_, n * sizeof(OrderEntry));
   return true;
 }
 

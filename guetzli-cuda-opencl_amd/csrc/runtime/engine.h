@@ -196,8 +196,11 @@ class Engine {
   // next OrderBuild, ahead of its weights).
   bool HasOrderCandidates() const { return ord_cand_n_ >= 0; }
   bool OrderReset();
+  // (entries: also fill and download the entries in the same synchronisation
+  // -- the common case, a radius with entries -- instead of OrderFetch)
   bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
-                  const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change);
+                  const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change,
+                  std::vector<std::pair<int, float>>* entries = nullptr);
   bool OrderFetch(std::pair<int, float>* out, size_t n);
   bool OrderAdvance(float val_threshold, int direction);
   // The back end's bulk prefix applied to the device copy (k_bulk_apply):
@@ -213,6 +216,8 @@ class Engine {
 
  private:
   Engine() = default;
+  bool OrderEntriesCapacity(size_t n);
+  bool OrderFillEnqueue(size_t grid_entries);
   bool Fail(const char* what, int code);
   void ProfBegin(const char* name);
   void ProfEnd();
