@@ -33,15 +33,31 @@ CASES = {
     "synth_1920x1080_s7_q95": (7, 1920, 1080, 95),
     # configs[4]: ~35 min of reference CPU time, ~7 GB host memory
     "synth_8192x8192_s0_q84": (0, 8192, 8192, 84),
+    # other qualities at 1080p, and gray content (R = G = B: the chroma the
+    # search sees is all zero, SaveToJpegData keeps one component) through
+    # the device bulk prefix and the tracked-histogram coder
+    "synth_1920x1080_s0_q90": (0, 1920, 1080, 90),
+    "gray_1920x1080_s0_q95": (0, 1920, 1080, 95, "gray"),
+    "gray_640x360_s3_q90": (3, 640, 360, 90, "gray"),
 }
+
+
+def case_rgb(seed, w, h, *mode):
+    """The case's input: the generator's frame, or its green channel in all
+    three (mode "gray")."""
+    rgb = guetzli_amd.synthetic_frame(seed, w, h)
+    if mode and mode[0] == "gray":
+        rgb = rgb.reshape(h, w, 3)[:, :, 1:2].repeat(3, axis=2).reshape(rgb.shape).copy()
+    return rgb
 
 
 def main():
     names = sys.argv[1:] or list(CASES)
     path = os.path.join(HERE, "manifest.json")
     for name in names:
-        seed, w, h, q = CASES[name]
-        rgb = guetzli_amd.synthetic_frame(seed, w, h).tobytes()
+        seed, w, h, q = CASES[name][:4]
+        mode = CASES[name][4:]
+        rgb = case_rgb(seed, w, h, *mode).tobytes()
         inp = "/tmp/gz_%s.rgb" % name
         open(inp, "wb").write(rgb)
         jpg = "/tmp/gz_%s.jpg" % name
@@ -49,7 +65,7 @@ def main():
                              capture_output=True, text=True)
         info = json.loads(res.stdout)
         entry = {
-            "seed": seed, "w": w, "h": h, "quality": q,
+            "seed": seed, "w": w, "h": h, "quality": q, **({"mode": mode[0]} if mode else {}),
             "input_sha256": hashlib.sha256(rgb).hexdigest(),
             "sha256": hashlib.sha256(open(jpg, "rb").read()).hexdigest(),
             "bytes": info["bytes"], "iters": info["iters"], "ref_seconds": info["seconds"]}

@@ -248,6 +248,8 @@ def test_process_reference_known_answers(gz, name):
 def test_process_synthetic_known_answers(gz, name):
     e = MANIFEST["synthetic"][name]
     rgb = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+    if e.get("mode") == "gray":  # (tests/golden/make_synthetic_fixtures.py case_rgb)
+        rgb = np.ascontiguousarray(rgb[:, :, 1:2].repeat(3, axis=2))
     assert hashlib.sha256(rgb.tobytes()).hexdigest() == e["input_sha256"]
     sha, stats = _jpeg_sha(gz, rgb, e["w"], e["h"], e["quality"])
     assert stats.iterations == e["iters"]

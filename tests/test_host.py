@@ -149,6 +149,8 @@ def test_synthetic_frames_deterministic(gz):
         if e["w"] * e["h"] > 640 * 360:
             continue
         f = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+        if e.get("mode") == "gray":  # (make_synthetic_fixtures.py case_rgb)
+            f = np.ascontiguousarray(f[:, :, 1:2].repeat(3, axis=2))
         assert f.shape == (e["h"], e["w"], 3)
         assert hashlib.sha256(f.tobytes()).hexdigest() == e["input_sha256"], name
         assert f.min() >= 16 and f.max() <= 240
