@@ -1208,7 +1208,7 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 // stream synchronisation.
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, info, arr, mbe, last, first, bytes;
+  size_t weight, active, cnt, off, info, arr, mbe, last, first, part, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
@@ -1220,7 +1220,8 @@ struct OrdLayout {
     mbe = arr + ((n / 256 / 64 + 2) * 4 + 255) / 256 * 256;
     last = mbe + a;
     first = last + a;  // the fill's tile starts: (entries <= 193 n) / 256 + 1 <= n + 4
-    bytes = first + ((n + 4) * 4 + 255) / 256 * 256;
+    part = first + ((n + 4) * 4 + 255) / 256 * 256;  // 2 ints per counting workgroup
+    bytes = part + ((n / 256 + 2) * 8 + 255) / 256 * 256;
   }
 };
 }  // namespace
@@ -1272,7 +1273,7 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   float* weight = reinterpret_cast<float*>(base + L.weight);
   int* active = reinterpret_cast<int*>(base + L.active);
   const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, direction,
-                    reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.info),
+                    reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.part),
                     reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
   const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
   int adv_dir = 0;
@@ -1339,7 +1340,7 @@ bool Engine::OrderFillEnqueue(size_t grid_entries) {
   int* off = reinterpret_cast<int*>(base + L.off);
   int* first = reinterpret_cast<int*>(base + L.first);
   const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_,
-                    ord_cand_n_, ord_direction_, cnt, reinterpret_cast<int*>(base + L.info),
+                    ord_cand_n_, ord_direction_, cnt, reinterpret_cast<int*>(base + L.part),
                     reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
   if (!ScanCounts(cnt, nb_, off, "order_scan", first)) return false;
   if (grid_entries == 0) return true;
