@@ -1102,12 +1102,19 @@ static size_t BzLdsPad() {
 }
 
 // offsets[0..n] = exclusive prefix sums of the device counts[0..n), on the stream.
-bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first) {
+bool Engine::ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first,
+                        const int* wg_totals) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (n > nb_) return Fail("ScanCounts size", 0);
   const unsigned chunks = static_cast<unsigned>((n + kScanChunk - 1) / kScanChunk);
+  if (wg_totals) {
+    // (per 256 counts, stride 2: k_order_local / k_order_near's partials)
+    GZ_TIMED(name, k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, wg_totals, 2, kScanChunk / 256, offsets,
+                                                         first));
+    return true;
+  }
   GZ_TIMED(name, (k_chunk_sums<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_),
-                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, offsets, first)));
+                  k_scan_chunks<<<chunks, 256, 0, s>>>(counts, n, d_scan_sums_, 1, 1, offsets, first)));
   return true;
 }
 
@@ -1342,7 +1349,9 @@ bool Engine::OrderFillEnqueue(size_t grid_entries) {
   const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_,
                     ord_cand_n_, ord_direction_, cnt, reinterpret_cast<int*>(base + L.part),
                     reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
-  if (!ScanCounts(cnt, nb_, off, "order_scan", first)) return false;
+  // (the chunk totals from the counting launch's per-workgroup entry totals)
+  if (!ScanCounts(cnt, nb_, off, "order_scan", first, reinterpret_cast<const int*>(base + L.part) + 1))
+    return false;
   if (grid_entries == 0) return true;
   GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((grid_entries + 255) / 256), 256, 0, s>>>(
       reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,

@@ -181,7 +181,10 @@ class Engine {
   bool JpegFetchPart(bool kept, std::vector<uint32_t>* words, ScanPart* part);
   // offsets[i] = counts[0] + ... + counts[i - 1] on the device (n + 1
   // entries); first (optional): the index holding element 256 c, per c
-  bool ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first = nullptr);
+  // wg_totals (optional): the totals of every 256 counts at stride 2 (a
+  // counting kernel's partials) -- the chunk sums without a launch
+  bool ScanCounts(const int* counts, int n, int* offsets, const char* name, int* first = nullptr,
+                  const int* wg_totals = nullptr);
   bool OrderBlocks(int comp_mask);
 
   // The search back end's change order on the device (SelectFrequencyBackEnd,
