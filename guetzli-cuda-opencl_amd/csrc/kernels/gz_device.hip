@@ -617,7 +617,7 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_,
                   d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_cbreq_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_};
+                  d_zero_bins_, d_scan_sums_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (void* g : compare_graph_)
@@ -635,6 +635,7 @@ Engine::~Engine() {
   if (h_delta_val_) hipHostFree(h_delta_val_);
   if (h_ord_) hipHostFree(h_ord_);
   if (h_ord_entries_) hipHostFree(h_ord_entries_);
+  if (h_cbreq_) (void)hipHostFree(h_cbreq_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
 
@@ -991,6 +992,58 @@ bool Engine::StartBlockComparisons(float* mask_scale_host) {
   return true;
 }
 
+// The per-request staging of CompareBlocks / CompareBlocksRgb: mapped pinned
+// host memory the kernel reads the request from and writes the errors to, so
+// a call is one launch and one wait (the comparator-level adapter makes one
+// call per CompareBlock; three copy blits per call cost more than the kernel).
+char* Engine::RequestStaging(size_t need, char** mapped) {
+  if (need > cbreq_cap_) {
+    if (h_cbreq_) {
+      if (hipStreamSynchronize(static_cast<hipStream_t>(stream_)) != hipSuccess) return nullptr;
+      (void)hipHostFree(h_cbreq_);
+    }
+    h_cbreq_ = nullptr;
+    m_cbreq_ = nullptr;
+    cbreq_cap_ = 0;
+    const size_t cap = std::max<size_t>(need, 4096);
+    if (hipHostMalloc(reinterpret_cast<void**>(&h_cbreq_), cap, hipHostMallocCoherent) != hipSuccess) {
+      h_cbreq_ = nullptr;
+      return nullptr;
+    }
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&m_cbreq_), h_cbreq_, 0) != hipSuccess) return nullptr;
+    cbreq_cap_ = cap;
+  }
+  *mapped = m_cbreq_;
+  return h_cbreq_;
+}
+
+// A single request's error, posted by k_compare_block1(_rgb) into the first
+// word of the staging buffer: the host polls it (the value replaces a NaN
+// pattern no comparison yields), checking the stream now and then so a failed
+// launch ends the wait.
+static constexpr uint64_t kNoResult = ~0ull;
+bool Engine::AwaitPosted(const char* h, double* err) {
+  const volatile uint64_t* slot = reinterpret_cast<const volatile uint64_t*>(h);
+  for (unsigned i = 1;; ++i) {
+    uint64_t v = *slot;
+    if (v != kNoResult) {
+      memcpy(err, &v, 8);
+      return true;
+    }
+    if ((i & 255) == 0) {
+      const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(stream_));
+      if (q == hipSuccess) {
+        v = *slot;
+        if (v == kNoResult) return Fail("CompareBlock: no result posted", 0);
+        memcpy(err, &v, 8);
+        return true;
+      }
+      if (q != hipErrorNotReady) return Fail("CompareBlock", q);
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 bool Engine::CompareBlocks(int n, const int* blocks, const int16_t* cand, double* err) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
@@ -998,27 +1051,34 @@ bool Engine::CompareBlocks(int n, const int* blocks, const int16_t* cand, double
   for (int i = 0; i < n; ++i)
     if (blocks[i] < 0 || blocks[i] >= nb_) return Fail("CompareBlocks block index", 0);
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
-  // one staging buffer: block indices | candidates | errors
-  const size_t need = static_cast<size_t>(n) * (4 + 192 * 2 + 8) + 64;
-  if (need > cbreq_cap_) {
-    GZ_HIP(hipStreamSynchronize(s));
-    if (d_cbreq_) GZ_HIP(hipFree(d_cbreq_));
-    d_cbreq_ = nullptr;
-    cbreq_cap_ = 0;
-    GZ_HIP(hipMalloc(&d_cbreq_, need));
-    cbreq_cap_ = need;
+  if (n == 1) {
+    char* m = nullptr;
+    char* h = RequestStaging(64, &m);
+    if (!h) return Fail("CompareBlocks staging", 0);
+    CompareRequest q;
+    q.block = blocks[0];
+    memcpy(q.cand, cand, sizeof(q.cand));
+    *reinterpret_cast<volatile uint64_t*>(h) = kNoResult;
+    GZ_TIMED("compare_blocks", k_compare_block1<<<1, 64, 0, s>>>(q, d_rgb_, d_mask_scale_, w_, h_, bw_,
+                                                                  reinterpret_cast<double*>(m)));
+    if (!AwaitPosted(h, err)) return false;
+    ProfFlush();
+    return true;
   }
-  char* base = static_cast<char*>(d_cbreq_);
-  int* d_blocks = reinterpret_cast<int*>(base);
-  int16_t* d_cand = reinterpret_cast<int16_t*>(base + ((static_cast<size_t>(n) * 4 + 15) & ~15ull));
-  double* d_err = reinterpret_cast<double*>(
-      reinterpret_cast<char*>(d_cand) + ((static_cast<size_t>(n) * 384 + 15) & ~15ull));
-  GZ_HIP(hipMemcpyAsync(d_blocks, blocks, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
-  GZ_HIP(hipMemcpyAsync(d_cand, cand, static_cast<size_t>(n) * 384, hipMemcpyHostToDevice, s));
-  GZ_TIMED("compare_blocks", k_compare_blocks<<<n, 64, 0, s>>>(d_blocks, d_cand, n, d_rgb_, d_mask_scale_,
-                                                                w_, h_, bw_, d_err));
-  GZ_HIP(hipMemcpyAsync(err, d_err, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s));
+  // one staging buffer: block indices | candidates | errors
+  const size_t o_cand = (static_cast<size_t>(n) * 4 + 15) & ~15ull;
+  const size_t o_err = o_cand + ((static_cast<size_t>(n) * 384 + 15) & ~15ull);
+  char* m = nullptr;
+  char* h = RequestStaging(o_err + static_cast<size_t>(n) * 8, &m);
+  if (!h) return Fail("CompareBlocks staging", 0);
+  memcpy(h, blocks, static_cast<size_t>(n) * 4);
+  memcpy(h + o_cand, cand, static_cast<size_t>(n) * 384);
+  GZ_TIMED("compare_blocks", k_compare_blocks<<<n, 64, 0, s>>>(reinterpret_cast<const int*>(m),
+                                                                reinterpret_cast<const int16_t*>(m + o_cand), n,
+                                                                d_rgb_, d_mask_scale_, w_, h_, bw_,
+                                                                reinterpret_cast<double*>(m + o_err)));
   GZ_HIP(hipStreamSynchronize(s));
+  memcpy(err, h + o_err, static_cast<size_t>(n) * 8);
   ProfFlush();
   return true;
 }
@@ -1039,27 +1099,34 @@ bool Engine::CompareBlocksRgb(int n, const int* blocks, const uint8_t* rgb, doub
   for (int i = 0; i < n; ++i)
     if (blocks[i] < 0 || blocks[i] >= nb_) return Fail("CompareBlocksRgb block index", 0);
   if (!have_mask_scale_ && !StartBlockComparisons(nullptr)) return false;
-  // one staging buffer: block indices | windows | errors
-  const size_t need = static_cast<size_t>(n) * (4 + 192 + 8) + 64;
-  if (need > cbreq_cap_) {
-    GZ_HIP(hipStreamSynchronize(s));
-    if (d_cbreq_) GZ_HIP(hipFree(d_cbreq_));
-    d_cbreq_ = nullptr;
-    cbreq_cap_ = 0;
-    GZ_HIP(hipMalloc(&d_cbreq_, need));
-    cbreq_cap_ = need;
+  if (n == 1) {
+    char* m = nullptr;
+    char* h = RequestStaging(64, &m);
+    if (!h) return Fail("CompareBlocksRgb staging", 0);
+    CompareRequestRgb q;
+    q.block = blocks[0];
+    memcpy(q.rgb, rgb, sizeof(q.rgb));
+    *reinterpret_cast<volatile uint64_t*>(h) = kNoResult;
+    GZ_TIMED("compare_blocks_rgb", k_compare_block1_rgb<<<1, 64, 0, s>>>(q, d_rgb_, d_mask_scale_, w_, h_, bw_,
+                                                                          reinterpret_cast<double*>(m)));
+    if (!AwaitPosted(h, err)) return false;
+    ProfFlush();
+    return true;
   }
-  char* base = static_cast<char*>(d_cbreq_);
-  int* d_blocks = reinterpret_cast<int*>(base);
-  uint8_t* d_rgb = reinterpret_cast<uint8_t*>(base + ((static_cast<size_t>(n) * 4 + 15) & ~15ull));
-  double* d_err = reinterpret_cast<double*>(
-      reinterpret_cast<char*>(d_rgb) + ((static_cast<size_t>(n) * 192 + 15) & ~15ull));
-  GZ_HIP(hipMemcpyAsync(d_blocks, blocks, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
-  GZ_HIP(hipMemcpyAsync(d_rgb, rgb, static_cast<size_t>(n) * 192, hipMemcpyHostToDevice, s));
-  GZ_TIMED("compare_blocks_rgb", k_compare_blocks_rgb<<<n, 64, 0, s>>>(d_blocks, d_rgb, n, d_rgb_, d_mask_scale_,
-                                                                        w_, h_, bw_, d_err));
-  GZ_HIP(hipMemcpyAsync(err, d_err, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s));
+  // one staging buffer: block indices | windows | errors
+  const size_t o_rgb = (static_cast<size_t>(n) * 4 + 15) & ~15ull;
+  const size_t o_err = o_rgb + ((static_cast<size_t>(n) * 192 + 15) & ~15ull);
+  char* m = nullptr;
+  char* h = RequestStaging(o_err + static_cast<size_t>(n) * 8, &m);
+  if (!h) return Fail("CompareBlocksRgb staging", 0);
+  memcpy(h, blocks, static_cast<size_t>(n) * 4);
+  memcpy(h + o_rgb, rgb, static_cast<size_t>(n) * 192);
+  GZ_TIMED("compare_blocks_rgb",
+           k_compare_blocks_rgb<<<n, 64, 0, s>>>(reinterpret_cast<const int*>(m),
+                                                 reinterpret_cast<const uint8_t*>(m + o_rgb), n, d_rgb_,
+                                                 d_mask_scale_, w_, h_, bw_, reinterpret_cast<double*>(m + o_err)));
   GZ_HIP(hipStreamSynchronize(s));
+  memcpy(err, h + o_err, static_cast<size_t>(n) * 8);
   ProfFlush();
   return true;
 }

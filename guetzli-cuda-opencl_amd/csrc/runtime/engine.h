@@ -220,6 +220,8 @@ class Engine {
  private:
   Engine() = default;
   bool OrderEntriesCapacity(size_t n);
+  char* RequestStaging(size_t need, char** mapped);  // CompareBlocks* mapped staging
+  bool AwaitPosted(const char* h, double* err);
   bool OrderFillEnqueue(size_t grid_entries);
   bool Fail(const char* what, int code);
   void ProfBegin(const char* name);
@@ -309,7 +311,8 @@ class Engine {
   uint32_t* m_delta_idx_ = nullptr;   // ... their device-side (mapped) addresses
   int16_t* m_delta_val_ = nullptr;
   size_t delta_cap_ = 0;
-  void* d_cbreq_ = nullptr;  // CompareBlocks staging (indices | candidates | errors)
+  char* h_cbreq_ = nullptr;  // CompareBlocks staging, mapped (indices | candidates | errors)
+  char* m_cbreq_ = nullptr;
   size_t cbreq_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
