@@ -630,14 +630,48 @@ bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direct
   return true;
 }
 
+// The scan's bit count from the histograms the candidate is coded with:
+// every symbol's code length plus its extra bits (the DC category; an AC
+// symbol's low nibble).  Without the 0xff stuffing and the padding this is
+// what k_jpeg_code counts, so prologue + ceil(bits / 8) + EOI bounds the
+// candidate's size from below.
+static uint64_t ScanBits(const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
+                         const JpegCodeTables& codes) {
+  uint64_t bits = 0;
+  for (int c = 0; c < ncomp; ++c)
+    for (int i = 0; i < 256; ++i) {
+      // (the counts are stored doubled, JpegHistogram::Add)
+      bits += static_cast<uint64_t>(dc[c].counts[i] / 2) * (codes.dc_len[c][i] + i);
+      bits += static_cast<uint64_t>(ac[c].counts[i] / 2) * (codes.ac_len[c][i] + (i & 15));
+    }
+  return bits;
+}
+
+// The distance at and above which ScoreJPEG(distance, size, target) >= best
+// for every size >= size_lb (processor.cc:151-160 keeps a candidate only
+// when its score is below the best; ScoreJPEG, score.cc:23-34, grows with the
+// distance and with the size), with a margin; -inf when no size from size_lb
+// up can beat best at any distance.
+static double HopelessDistance(double best, size_t size_lb, double target) {
+  const double s = static_cast<double>(size_lb);
+  if (s >= best) return -HUGE_VAL;
+  const double kScale = 50, kMaxExponent = 10, kLargeSize = 1e30;
+  double diff = std::log(best / s) / kScale;  // exp(kScale * diff) * size_lb >= best
+  if (diff > kMaxExponent / kScale)           // above it the linear branch decides
+    diff = std::max(kMaxExponent / kScale, (best - s) / (kLargeSize * std::exp(kMaxExponent)));
+  return target + diff + 1e-6;
+}
+
 bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta,
                                                            bool strip_metadata, const JpegHistogram dc[3],
                                                            const JpegHistogram ac[3], int ncomp,
-                                                           size_t* size) {
+                                                           double best_score, size_t* size, bool* skipped) {
   // the Compare pass first; the codes on the host while it runs; the scan
-  // behind it; one wait
+  // behind it (not coded when the pass's distance shows the candidate
+  // cannot become the output); one wait
   const auto t0 = Clock::now();
   const double c0 = ThreadCpu();
+  *skipped = false;
   if (!SyncCoeffs(img)) return false;
   Engine* e = engine_.get();
   if (!e->CompareEnqueue()) {
@@ -654,15 +688,26 @@ bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img
     err_ = "jpeg header";
     return false;
   }
+  const uint64_t bound_bits = ScanBits(dc, ac, ncomp, codes);
+  const size_t size_lb = cur_prologue_.size() + static_cast<size_t>((bound_bits + 7) / 8) + 2;
+  float skip_at = HUGE_VALF;
+  if (best_score >= 0 && scan_bound_mismatches == 0) {
+    const double d = HopelessDistance(best_score, size_lb, target_);
+    if (d <= -HUGE_VAL) {
+      skip_at = -HUGE_VALF;
+    } else if (d < 1e30) {
+      skip_at = std::nextafter(static_cast<float>(d), HUGE_VALF);
+    }
+  }
   seconds_encode += Since(t0);
   uint64_t nbits = 0, ff = 0;
-  if (!e->JpegScanEnqueue(ncomp, img.quant, codes)) {
+  if (!e->JpegScanEnqueue(ncomp, img.quant, codes, skip_at)) {
     err_ = e->error();
     return false;
   }
   const auto tw = Clock::now();
   const double cw = ThreadCpu();
-  if (!e->Sync() || !e->JpegScanFinish(&nbits, &ff)) {
+  if (!e->Sync()) {
     err_ = e->error();
     return false;
   }
@@ -671,6 +716,25 @@ bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img
   (void)e->CompareFinish(&distance_, nullptr);
   block_max_stale_ = true;
   ++compares;
+  if (distance_ >= skip_at) {  // (k_jpeg_code's own test, on the same float)
+    if (ScoreJPEG(distance_, static_cast<int>(size_lb), target_) >= best_score) {
+      *skipped = true;
+      ++scans_skipped;
+      seconds_compare += Since(t0);
+      cpu_compare += ThreadCpu() - c0;
+      return true;
+    }
+    // (the margin makes this unreachable; code the scan after all)
+    if (!e->JpegScanEnqueue(ncomp, img.quant, codes) || !e->Sync()) {
+      err_ = e->error();
+      return false;
+    }
+  }
+  if (!e->JpegScanFinish(&nbits, &ff)) {
+    err_ = e->error();
+    return false;
+  }
+  if (nbits != bound_bits) ++scan_bound_mismatches;
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((nbits + 7) / 8 + ff) + 2;
   *size = cur_size_;
   seconds_compare += Since(t0);
@@ -1441,14 +1505,19 @@ class Processor {
     JpegHistogram ach[3];
     for (int c = 0; c < ncomp && c < static_cast<int>(ac.size()); ++c) ach[c] = ac[c];
     size_t size = 0;
-    if (!cmp_->DeviceEncodeAndCompareKnown(img, jpg, params_.clear_metadata, dc0, ach, ncomp, &size))
+    bool skipped = false;
+    // (FlushOutput above: final_score_ includes every earlier candidate)
+    if (!cmp_->DeviceEncodeAndCompareKnown(img, jpg, params_.clear_metadata, dc0, ach, ncomp, final_score_, &size,
+                                           &skipped))
       return Fail(err);
     pending_.clear();
     pending_size_ = size;
     has_pending_ = true;
     pending_device_ = true;
+    pending_skipped_ = skipped;
     res_->detail["encode_compare_s"] += Since(t0);
     res_->detail["encode_known_histograms"] += 1;
+    if (skipped) res_->detail["scans_skipped"] += 1;
     return true;
   }
   // Joins the pending encode and applies its MaybeOutput; returns its size.
@@ -1463,6 +1532,10 @@ class Processor {
       res_->detail["write_encode_s"] += encode_s_;
     }
     has_pending_ = false;
+    if (pending_skipped_) {  // its score is not below final_score_: MaybeOutput keeps nothing
+      pending_skipped_ = false;
+      return 0;
+    }
     if (pending_device_) {
       MaybeOutputDevice(pending_size_);
       return pending_size_;
@@ -1530,6 +1603,7 @@ class Processor {
   std::string pending_;
   bool has_pending_ = false;
   bool pending_device_ = false;
+  bool pending_skipped_ = false;  // a back-end candidate that could not win, not coded
   size_t pending_size_ = 0;
   bool kept_on_device_ = false;  // the best candidate so far is the device's kept slot
   size_t best_size_ = 0;
@@ -2808,6 +2882,7 @@ int Process(int device, const ProcessParams& params, const uint8_t* rgb, bool de
     result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
     result->detail["compare_wait_s"] = cmp->seconds_wait;
     result->detail["compare_wait_cpu_s"] = cmp->cpu_wait;
+    result->detail["scan_bound_mismatches"] = cmp->scan_bound_mismatches;
   }
   result->seconds_total = Since(t0);
   result->detail["thread_cpu_s"] = ThreadCpu() - c0;
@@ -2868,6 +2943,7 @@ int ProcessJpeg(int device, const ProcessParams& params, const uint8_t* data, si
     result->detail["compare_thread_cpu_s"] = cmp->cpu_compare;
     result->detail["compare_wait_s"] = cmp->seconds_wait;
     result->detail["compare_wait_cpu_s"] = cmp->cpu_wait;
+    result->detail["scan_bound_mismatches"] = cmp->scan_bound_mismatches;
   }
   result->seconds_total = Since(t0);
   result->detail["thread_cpu_s"] = ThreadCpu() - c0;

@@ -122,10 +122,13 @@ class Comparator {
   // histograms SaveToJpegData + WriteJpeg would count (comps at or above
   // ncomp cleared), so the device only codes the scan -- no histogram pass,
   // no wait for one.  HasKnownHistogramEncode() false: not supported.
+  // best_score >= 0: the score the candidate must beat to become the output
+  // (MaybeOutput); when its distance and a lower bound of its size show it
+  // cannot, the scan is not coded and *skipped is set (*size undefined).
   virtual bool HasKnownHistogramEncode() const { return false; }
   virtual bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                                            const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
-                                           size_t* size) {
+                                           double best_score, size_t* size, bool* skipped) {
     return false;
   }
   // The back end's bulk prefix on the device (with the device order only):
@@ -247,7 +250,7 @@ class HipButteraugliComparator : public Comparator {
   bool HasKnownHistogramEncode() const override { return true; }
   bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                                    const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
-                                   size_t* size) override;
+                                   double best_score, size_t* size, bool* skipped) override;
   bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   bool SetOriginalCoeffs420(const JpegData& jpg420) override;
@@ -267,6 +270,10 @@ class HipButteraugliComparator : public Comparator {
   double seconds_zeroing = 0.0;
   double seconds_bulk = 0.0;  // DeviceBulkApply (wall)
   int compares = 0;
+  int scans_skipped = 0;  // back-end candidates not coded (DeviceEncodeAndCompareKnown)
+  // coded back-end scans whose bit count differed from the histogram bound
+  // (never expected; the first one turns the skipping off)
+  int scan_bound_mismatches = 0;
 
  private:
   bool SyncCoeffs(const CoeffImage& img);

@@ -1600,12 +1600,12 @@ bool Engine::JpegScan(int ncomp, const int q[3][64], const JpegCodeTables& codes
 
 // (the caller has synchronised since the previous scan: the pinned code
 // staging is free)
-bool Engine::JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes) {
-  return JpegScanEnqueueRange(ncomp, q, codes, 0, nb_, 0, true);
+bool Engine::JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes, float skip_at) {
+  return JpegScanEnqueueRange(ncomp, q, codes, 0, nb_, 0, true, skip_at);
 }
 
 bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeTables& codes, int m0, int m1,
-                                  uint64_t base, bool pad_end) {
+                                  uint64_t base, bool pad_end, float skip_at) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ncomp < 1 || ncomp > 3) return Fail("JpegScan component count", 0);
@@ -1644,7 +1644,8 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
                                                             static_cast<unsigned long long>(base),
                                                             pad_end ? 1 : 0, words, ffc, arr, status, side,
-                                                            seam, jepoch_, m_jhist_ + 6 * 256 + 2));
+                                                            seam, jepoch_, m_jhist_ + 6 * 256 + 2,
+                                                            d_dmax_ + kDistWord, skip_at));
   jpart_[jslot_].base = base;
   // (0xff count, bit total, shared words) reach h_jhist_[1538..1543] from
   // the last workgroup to finish

@@ -152,7 +152,11 @@ class Engine {
   bool JpegStageEnqueue(const int q[3][64]);
   bool JpegStageWait(uint32_t* hist, uint64_t* chroma_nz);
   bool CompareEnqueue();
-  bool JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes);
+  // skip_at: the scan is not coded when the distance of the Compare pass
+  // queued before it is at or above skip_at (the caller knows the candidate
+  // cannot become the output; JpegScanFinish must not be called then).
+  bool JpegScanEnqueue(int ncomp, const int q[3][64], const JpegCodeTables& codes,
+                       float skip_at = __builtin_inff());
   bool Sync();
   // distance: the pass's maximum (from mapped memory); block_max (may be
   // null): the per-block maxima, copied from HBM.
@@ -174,7 +178,7 @@ class Engine {
   };
   bool JpegStageEnqueueRange(const int q[3][64], int m0, int m1);
   bool JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeTables& codes, int m0, int m1,
-                            uint64_t base, bool pad_end);
+                            uint64_t base, bool pad_end, float skip_at = __builtin_inff());
   bool JpegScanFinishPart(ScanPart* part);
   // The stored words of a slot's part (memory byte order; words[0] is the
   // stream's word base >> 5, the shared ones zero) and its ScanPart.

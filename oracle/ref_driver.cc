@@ -108,6 +108,7 @@ int Encode(int argc, char** argv) {
     else return 1;
   }
   guetzli::ProcessStats stats;
+  if (getenv("GZ_REF_LOG")) stats.debug_output_file = stderr;  // the search's per-iteration log
   std::string out;
   auto t0 = std::chrono::steady_clock::now();
   bool ok = guetzli::Process(params, &stats, rgb, w, h, &out);

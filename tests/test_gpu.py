@@ -232,6 +232,10 @@ def test_coder_forward_progress_under_occupancy(gz, spare_xcd):
 
 def _jpeg_sha(gz, rgb, w, h, q):
     data, stats = gz.process(rgb, w, h, gz.Params.for_quality(q), return_stats=True)
+    # back-end candidates that cannot win are not coded; the size bound they
+    # are judged by is the coder's exact bit count for every coded one
+    detail = gz.last_process_detail()
+    assert detail.get("scan_bound_mismatches", 0) == 0, detail
     return hashlib.sha256(data).hexdigest(), stats
 
 
@@ -242,6 +246,10 @@ def test_process_reference_known_answers(gz, name):
     sha, stats = _jpeg_sha(gz, rgb, e["w"], e["h"], e["quality"])
     assert stats.iterations == e["iters"]
     assert sha == e["sha256"]
+    if name == "bees_q90":
+        # (the reference's log of this search: 19 of its 21 back-end
+        # candidates score far above the best output so far)
+        assert gz.last_process_detail().get("scans_skipped", 0) >= 10
 
 
 @pytest.mark.parametrize("name", sorted(MANIFEST.get("synthetic", {})))
