@@ -796,7 +796,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // S1-S3: opsin dynamics (blur + transform) and high intensity change
   // masking, fused
   {
-    const int rows = OpsinStreamRows(w_, h_);
+    static const int env_rows = getenv("GZ_OPSIN_ROWS") ? atoi(getenv("GZ_OPSIN_ROWS")) : 0;
+    const int rows = env_rows > 0 ? env_rows : OpsinStreamRows(w_, h_);
     const int strips = (w_ + kOsCols - 1) / kOsCols, segs = (h_ + rows - 1) / rows;
     float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
     GZ_TIMED("opsin_mhic", k_opsin_mhic_stream<<<(strips * segs + 3) / 4, 256, 0, s>>>(
@@ -810,7 +811,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // mask front, fused (one read of m0 / m1): blurred planes -> d_bl_, mask
   // front -> d_mb_ (consumed by the mask blurs below)
   {
-    const int rows = EdgeMaskRows(w_, h_);
+    static const int env_rows = getenv("GZ_EDGE_ROWS") ? atoi(getenv("GZ_EDGE_ROWS")) : 0;
+    const int rows = env_rows > 0 ? env_rows : EdgeMaskRows(w_, h_);
     const int strips = (w_ + kEmCols - 1) / kEmCols, segs = (h_ + rows - 1) / rows;
     const int waves = 3 * strips * segs;
     GZ_TIMED("edge_mask", k_edge_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(
