@@ -410,15 +410,6 @@ __device__ __forceinline__ int pixel_byte(unsigned p, int x) { return ((p + 8 - 
 // (color_transform.h tables): 1.40200, 1.77200, 0.71414, 0.34414.
 constexpr int kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554;
 
-__device__ __forceinline__ void ycbcr_to_linear(int y, int cb, int cr, float out[3]) {
-  const int r = clamp255(y + c_tab.cr_r[cr]);
-  const int g = clamp255(y + ((c_tab.cr_g[cr] + c_tab.cb_g[cb]) >> 16));
-  const int b = clamp255(y + c_tab.cb_b[cb]);
-  out[0] = c_tab.srgb[r];
-  out[1] = c_tab.srgb[g];
-  out[2] = c_tab.srgb[b];
-}
-
 // ---------------------------------------------------------------------------
 // Mask LUT stage at one pixel (MaskOpt tail, :1234-1263)
 // ---------------------------------------------------------------------------
