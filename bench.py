@@ -66,8 +66,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # read it and write 1/step^2).  Derivation in DESIGN.md §4.
 def stage_bytes_per_px():
     s = {}
-    s["coeffs_to_linear"] = 3 * 2 + 3 * 4          # int16 coeffs -> 3 f32 planes
-    s["opsin_mhic"] = 3 * 4 + 3 * 4 + 6 * 4          # S1-S3 fused: linear + ref XYB -> m0, m1
+    s["coeffs_to_linear"] = 3 * 2 + 4              # int16 coeffs -> packed sRGB bytes (4 B/px)
+    s["opsin_mhic"] = 4 + 3 * 4 + 6 * 4              # S1-S3 fused: sRGB bytes + ref XYB -> m0, m1
     s["edge_blur"] = 6 * 4 + 6 * 4                  # S4: 6 separable blurs, 6 -> 6
     s["edge_mask"] = 6 * 4 + 6 * 4 + 3 * 4          # S4 + S9-S11 fused: 6 -> 6 blurred + 3 mask front
     s["edge_map"] = 6 * 4 + 3 * 4 / 9.0              # (stage dumps only; fused into block_diff)
@@ -145,7 +145,7 @@ BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "d
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
 STAGE_SYMBOL = {
-    "coeffs_to_linear": "gz::k_coeffs_to_linear(", "opsin_mhic": "gz::k_opsin_mhic_stream(",
+    "coeffs_to_linear": "gz::k_coeffs_to_srgb8(", "opsin_mhic": "gz::k_opsin_mhic_stream(",
     "edge_blur": "void gz::k_blur_stream<2>(", "edge_map": "gz::k_edge_map(",
     "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
     "lowfreq_blur_v": "void gz::k_blur_vstream<3>(", "low_freq": "gz::k_low_freq(",

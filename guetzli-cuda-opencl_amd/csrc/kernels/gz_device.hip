@@ -417,6 +417,7 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_cur_), nc * sizeof(int16_t));
   alloc(reinterpret_cast<void**>(&e->d_ref_xyb_), 3 * n * 4);
   alloc(reinterpret_cast<void**>(&e->d_lin_), 3 * n * 4);
+  alloc(reinterpret_cast<void**>(&e->d_px8_), n * 4);
   alloc(reinterpret_cast<void**>(&e->d_xyb_), 3 * n * 4);
   alloc(reinterpret_cast<void**>(&e->d_m0_), 3 * n * 4);
   alloc(reinterpret_cast<void**>(&e->d_m1_), 3 * n * 4);
@@ -617,7 +618,7 @@ Engine::~Engine() {
                   d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_,
                   d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
-                  d_zero_bins_, d_scan_sums_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_};
+                  d_zero_bins_, d_scan_sums_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_, d_px8_};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (void* g : compare_graph_)
@@ -785,14 +786,17 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     GZ_HIP(hipMemsetAsync(d_dc_, 0, 3 * rn * 4, s));
     GZ_HIP(hipMemsetAsync(d_ac_, 0, 3 * rn * 4, s));
   }
-  // S0: candidate coefficients -> linear RGB
+  // S0: candidate coefficients -> sRGB pixels (packed)
   if (cand_src_ == kCandRgb) {
-    GZ_TIMED("rgb_to_linear", k_rgb_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_cand_rgb_, n_, d_lin_));
+    GZ_TIMED("rgb_to_linear", k_rgb_to_srgb8<<<(n_ + 255) / 256, 256, 0, s>>>(d_cand_rgb_, n_, d_px8_));
   } else {
-    GZ_TIMED("coeffs_to_linear", k_coeffs_to_linear<<<dim3((bw_ + kC2lBlocks - 1) / kC2lBlocks, bh_), 256, 0, s>>>(
-        d_cur_, w_, h_, bw_, nb_, d_lin_, cand_src_ == kCand420 ? d_planes_ : nullptr));
+    GZ_TIMED("coeffs_to_linear", k_coeffs_to_srgb8<<<dim3((bw_ + kC2lBlocks - 1) / kC2lBlocks, bh_), 256, 0, s>>>(
+        d_cur_, w_, h_, bw_, nb_, d_px8_, cand_src_ == kCand420 ? d_planes_ : nullptr));
   }
-  if (dbg && !d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
+  if (dbg && dbg->cand_linear) {
+    GZ_TIMED("srgb8_to_linear", k_srgb8_to_linear<<<(n_ + 255) / 256, 256, 0, s>>>(d_px8_, n_, d_lin_));
+    if (!d2h(dbg->cand_linear, d_lin_, 3 * n)) return false;
+  }
   // S1-S3: opsin dynamics (blur + transform) and high intensity change
   // masking, fused
   {
@@ -801,7 +805,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     const int strips = (w_ + kOsCols - 1) / kOsCols, segs = (h_ + rows - 1) / rows;
     float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
     GZ_TIMED("opsin_mhic", k_opsin_mhic_stream<<<(strips * segs + 3) / 4, 256, 0, s>>>(
-        d_lin_, d_ref_xyb_, w_, h_, strips, segs, rows, d_m0_, d_m1_, xyb_dbg, d_scales_,
+        d_px8_, d_ref_xyb_, w_, h_, strips, segs, rows, d_m0_, d_m1_, xyb_dbg, d_scales_,
         scale_stride_));
     if (xyb_dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   }

@@ -266,7 +266,8 @@ class Engine {
   int16_t* d_orig_ = nullptr;
   int16_t* d_cur_ = nullptr;
   float* d_ref_xyb_ = nullptr;
-  float* d_lin_ = nullptr;
+  float* d_lin_ = nullptr;    // the reference's linear planes (and the stage dumps')
+  uint32_t* d_px8_ = nullptr;  // the candidate's sRGB pixels, packed (the Compare pass's input)
   float* d_xyb_ = nullptr;
   float* d_m0_ = nullptr;
   float* d_m1_ = nullptr;
