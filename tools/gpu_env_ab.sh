@@ -1,7 +1,8 @@
 #!/bin/bash
 # Interleaved bench lines for environment settings of one build:
 #   bash tools/gpu_env_ab.sh "base:" "r16:GZ_OPSIN_ROWS=16" ...
-# (GZ_AB_RUNS rounds; per line: name, MP/s, ms/step, host CPU s/frame, bit-exact frames)
+# (GZ_AB_RUNS rounds; per line: name, MP/s, ms/step, host CPU s/frame, bit-exact frames,
+# the isolated frame's GPU regions, its wall seconds and host back-end seconds)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/envab
 mkdir -p $O
@@ -16,7 +17,9 @@ for r in $(seq ${GZ_AB_RUNS:-2}); do
 import json
 d = json.loads(open('$f.json').read().strip().splitlines()[-1])
 g = d.get('gpu_regions_ms_per_frame', {})
+sf = d.get('single_frame', {})
 print('$name', d['value'], d['ms_per_step'], d['host_cpu_seconds_per_frame'], d['verified']['bit_exact'],
-      {k: g.get(k) for k in '${GZ_AB_REGIONS:-opsin_mhic edge_mask blur_h blur_v}'.split()})"
+      {k: g.get(k) for k in '${GZ_AB_REGIONS:-opsin_mhic edge_mask blur_h blur_v}'.split()},
+      sf.get('seconds'), sf.get('host_breakdown_seconds', {}).get('seconds_backend'))"
   done
 done
