@@ -158,7 +158,18 @@ bool HipButteraugliComparator::IsOriginal(const CoeffImage& img) const {
 // journalled edits when it is in img's epoch, else everything.
 bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
   if (device_.Current(img)) return true;
-  const bool replay = device_.CanReplay(img) && img.changed.size() - device_.pos < img.coeffs.size() / 8;
+  // A short journal is replayed, a long one replaced by a full upload --
+  // except while the host copy is partial (the back end's lazily
+  // materialised blocks): then only the journalled values are current, so
+  // the journal is replayed whatever its length.  (GZ_REPLAY_DIV: the
+  // journal length above which the full upload is chosen, as a fraction
+  // 1/GZ_REPLAY_DIV of the coefficients; tests force long tails with it.)
+  static const size_t replay_div = [] {
+    const char* e = std::getenv("GZ_REPLAY_DIV");
+    return static_cast<size_t>(e && std::atoi(e) > 0 ? std::atoi(e) : 8);
+  }();
+  const bool short_journal = img.changed.size() - device_.pos < img.coeffs.size() / replay_div;
+  const bool replay = device_.CanReplay(img) && (short_journal || img.host_partial);
   if (!img.host_valid || (img.host_partial && !replay)) {
     err_ = "coefficients are current on neither side";
     return false;
@@ -188,9 +199,11 @@ bool HipButteraugliComparator::SyncCoeffs(const CoeffImage& img) {
 const std::vector<float>& HipButteraugliComparator::block_max_distance() const {
   if (block_max_stale_) {
     float d = 0.0f;
+    block_max_failed_ = false;
     if (engine_->CompareFinish(&d, block_max_.data())) {
       block_max_stale_ = false;
     } else {
+      block_max_failed_ = true;
       err_ = engine_->error();
       std::fill(block_max_.begin(), block_max_.end(), std::numeric_limits<float>::infinity());
     }
@@ -587,11 +600,14 @@ bool HipButteraugliComparator::BlockZeroingCandidates420(Image420* img, int comp
 bool HipButteraugliComparator::DeviceOrderReset(bool* available) {
   *available = false;
   if (!engine_->HasOrderCandidates()) return true;
-  if (!engine_->OrderReset()) {
+  // (an allocation failure leaves the order on the host; a stream or launch
+  // error fails the encode)
+  bool unavailable = false;
+  if (!engine_->OrderReset(&unavailable)) {
     err_ = engine_->error();
     return false;
   }
-  *available = true;
+  *available = !unavailable;
   return true;
 }
 
@@ -716,7 +732,7 @@ bool HipButteraugliComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img
   (void)e->CompareFinish(&distance_, nullptr);
   block_max_stale_ = true;
   ++compares;
-  if (distance_ >= skip_at) {  // (k_jpeg_code's own test, on the same float)
+  if (skip_at != HUGE_VALF && distance_ >= skip_at) {  // (k_jpeg_code's own test, on the same float)
     if (ScoreJPEG(distance_, static_cast<int>(size_lb), target_) >= best_score) {
       *skipped = true;
       ++scans_skipped;
@@ -1797,6 +1813,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         if (!cmp_->DeviceChangeOrder(direction, target_mul, first_up_iter, last_indexes, &global_order,
                                      &blocks_to_change))
           return Fail(err);
+      } else if (!first_up_iter && (cmp_->block_max_distance(), cmp_->block_max_failed())) {
+        return Fail(err);
       } else if (!BuildChangeOrder(direction, 1, target_mul, num_blocks, own_lo, own_hi, gbase,
                                    first_up_iter ? zero_block_max : cmp_->block_max_distance(), last_indexes,
                                    offsets, cand_err, max_block_error, &global_order, &block_weight,
@@ -2063,18 +2081,133 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             __builtin_prefetch(&acm.nz[static_cast<size_t>(c) * num_blocks + b], 1);
           }
         };
-        for (size_t i = bulk; i < n_order; ++i) {
-          if (i >= sorter->sorted()) {
-            const auto ts = Clock::now();
-            sorter->EnsureSorted(i);
-            sort_s += Since(ts);
+        // The tail in speculative batches.  The entropy codes read at change
+        // i (i % 10 == 0) are a function of the AC histograms after change i
+        // alone, and the histograms after every change follow from the
+        // changes' symbol updates, which need no codes.  So a batch applies
+        // its changes first (recording each one's symbol updates and what
+        // undoes it), copies the histograms at every step whose codes are
+        // read, builds those codes on the pool at once, then runs the
+        // estimate and the break test over the batch in order with the same
+        // values as the one-at-a-time loop; the changes past the break are
+        // undone.  Batches grow from 4 to kMaxDecades rebuilds (capped by
+        // the pool workers this encode may use), so a tail that stops early
+        // wastes at most a few rebuilds.
+        struct Spec {
+          int bix, c, k;
+          coeff_t old;
+          uint64_t nz;
+          float key;
+          SymbolLog log;
+        };
+        struct Snap {
+          size_t step;
+          JpegHistogram h[3];
+          std::vector<uint8_t> depths;
+          int size = 0;
+          int64_t raw[3] = {0, 0, 0};
+        };
+        std::vector<Spec> spec;
+        std::vector<Snap> snaps;
+        const int workers = std::max(1, PoolWorkerCap());
+        constexpr int kMaxDecades = 32;
+        // (GZ_SPEC_DECADES: a fixed batch, for A/B runs and tests)
+        static const int fixed_decades = getenv("GZ_SPEC_DECADES") ? std::max(1, atoi(getenv("GZ_SPEC_DECADES"))) : 0;
+        int decades = fixed_decades ? fixed_decades : std::min(4, 2 * workers);
+        size_t i = bulk;
+        bool stop = false;
+        while (!stop && i < n_order) {
+          const size_t first_code = (i + 9) / 10 * 10;
+          const size_t j = std::min(n_order, first_code + 10 * static_cast<size_t>(decades));
+          spec.clear();
+          size_t ns = 0;
+          // A: the batch's changes, their symbol updates into the histograms
+          for (size_t s = i; s < j; ++s) {
+            if (s >= sorter->sorted()) {
+              const auto ts = Clock::now();
+              sorter->EnsureSorted(s);
+              sort_s += Since(ts);
+            }
+            if (s >= prefetched) {
+              prefetched = std::max(sorter->sorted(), s + 1);
+              prefetch_chunk(s, std::min(prefetched, n_order));
+            }
+            const int bix = global_order[s].first;
+            if (device_bulk) materialize(bix);
+            const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
+            const int idx = cand[off + last_indexes[bix] + std::min(direction, 0)];
+            Spec sp;
+            sp.bix = bix;
+            sp.c = idx / kDCTBlockSize;
+            sp.k = idx % kDCTBlockSize;
+            sp.old = img->block(sp.c, bix)[sp.k];
+            sp.nz = acm.nz[static_cast<size_t>(sp.c) * num_blocks + bix];
+            sp.key = global_order[s].second;
+            apply(bix, &sp.log);
+            for (int e = 0; e < sp.log.n; ++e) ac_histograms[sp.c].Add(sp.log.sym[e], sp.log.weight[e]);
+            spec.push_back(sp);
+            if (loop.CodesRead(s)) {
+              if (ns == snaps.size()) snaps.emplace_back();
+              Snap& sn = snaps[ns++];
+              sn.step = s;
+              for (int c = 0; c < ncomp && c < 3; ++c) sn.h[c] = ac_histograms[c];
+            }
           }
-          if (i >= prefetched) {
-            prefetched = std::max(sorter->sorted(), i + 1);
-            prefetch_chunk(i, std::min(prefetched, n_order));
+          // B: the codes of every read step, on the pool (a task takes two
+          // consecutive ones: the code-length caches are per thread)
+          if (ns) {
+            const auto te = Clock::now();
+            const int tasks = static_cast<int>((ns + 1) / 2);
+            ParallelFor(tasks, [&](int t) {
+              for (size_t q = 2 * static_cast<size_t>(t); q < std::min(ns, 2 * static_cast<size_t>(t) + 2); ++q) {
+                Snap& sn = snaps[q];
+                std::vector<JpegHistogram> hv(sn.h, sn.h + ncomp);
+                sn.size = static_cast<int>(ComputeEntropyCodes(hv, &sn.depths));
+                for (int c = 0; c < ncomp; ++c)
+                  sn.raw[c] = HistogramRawBits(sn.h[c], &sn.depths[c * JpegHistogram::kSize]);
+              }
+            });
+            codes_s += Since(te);
+            n_codes += static_cast<int>(ns);
           }
-          apply(global_order[i].first, nullptr);
-          if (after_change(i, global_order[i].second)) break;
+          // C: the estimate and the break test in order
+          size_t q = 0, s = i;
+          for (; s < j; ++s) {
+            const Spec& sp = spec[s - i];
+            loop.Applied(sp.key);
+            if (q < ns && snaps[q].step == s) {
+              const Snap& sn = snaps[q++];
+              ac_histogram_size = sn.size;
+              ac_depths = sn.depths;
+              for (int c = 0; c < ncomp; ++c) raw_bits[c] = sn.raw[c];
+            } else {
+              const uint8_t* d = &ac_depths[sp.c * JpegHistogram::kSize];
+              for (int e = 0; e < sp.log.n; ++e)
+                raw_bits[sp.c] += static_cast<int64_t>(sp.log.weight[e]) * (d[sp.log.sym[e]] + (sp.log.sym[e] & 0xf));
+            }
+            if (!loop.EstimateRead(s)) continue;
+            est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
+            if (loop.Stop(est_jpg_size, prev_size)) {
+              stop = true;
+              break;
+            }
+          }
+          if (stop) {
+            // undo the changes after the break (newest first)
+            for (size_t u = j; u-- > s + 1;) {
+              const Spec& sp = spec[u - i];
+              img->block(sp.c, sp.bix)[sp.k] = sp.old;
+              acm.nz[static_cast<size_t>(sp.c) * num_blocks + sp.bix] = sp.nz;
+              last_indexes[sp.bix] -= direction;
+              if (device_bulk) mat_li[sp.bix] = last_indexes[sp.bix];
+              for (int e = 0; e < sp.log.n; ++e) ac_histograms[sp.c].Add(sp.log.sym[e], -sp.log.weight[e]);
+              // (its journal entry stays: it names a position whose value is current)
+            }
+            res_->detail["backend_spec_undone"] += static_cast<double>(j - s - 1);
+            res_->detail["backend_spec_wasted_codes"] += static_cast<double>(ns - q);
+          }
+          i = j;
+          if (!fixed_decades) decades = std::min(std::min(kMaxDecades, std::max(4, 2 * workers)), decades * 2);
         }
       } else {
         // The tail on a partitioned frame, a window of entries at a time: the
@@ -2738,6 +2871,7 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       std::vector<float> bmax(num_blocks, 0.0f);
       if (!first_up_iter) {
         const std::vector<float>& m8 = cmp_->block_max_distance();
+        if (cmp_->block_max_failed()) return Fail(err);
         const int bw8 = (w + 7) / 8, bh8 = (h + 7) / 8;
         for (int by = 0; by < bh8; ++by)
           for (int bx = 0; bx < bw8; ++bx) {

@@ -94,6 +94,9 @@ class Comparator {
   virtual bool DistanceOK(double target_mul) const = 0;
   virtual float distmap_aggregate() const = 0;
   virtual const std::vector<float>& block_max_distance() const = 0;
+  // True when the last block_max_distance() could not be formed (a failed
+  // device copy): its values are then not the maxima and error() says why.
+  virtual bool block_max_failed() const { return false; }
   virtual float BlockErrorLimit() const = 0;
   virtual void ComputeBlockErrorAdjustmentWeights(int direction, int max_block_dist,
                                                   double target_mul, int factor_x, int factor_y,
@@ -236,6 +239,7 @@ class HipButteraugliComparator : public Comparator {
   // (copied from the device on first use after a Compare: the device change
   // order reads them in HBM, so the search itself never asks)
   const std::vector<float>& block_max_distance() const override;
+  bool block_max_failed() const override { return block_max_failed_; }
   float BlockErrorLimit() const override { return target_; }
   void ComputeBlockErrorAdjustmentWeights(int direction, int max_block_dist, double target_mul,
                                           int factor_x, int factor_y,
@@ -301,6 +305,7 @@ class HipButteraugliComparator : public Comparator {
   float target_ = 0.0f;
   float distance_ = 0.0f;
   mutable std::vector<float> block_max_;
+  mutable bool block_max_failed_ = false;
   mutable bool block_max_stale_ = false;  // the last Compare's maxima are on the device only
   CoeffCursor device_;  // what the device copy of the coefficients reflects
   bool IsOriginal(const CoeffImage& img) const;

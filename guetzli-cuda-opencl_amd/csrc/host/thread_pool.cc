@@ -179,6 +179,9 @@ int UsableCpus(int* affinity, int* online) {
 }
 }  // namespace
 
+int ActiveEncodes() { return g_active_encodes.load(std::memory_order_relaxed); }
+int PoolWorkerCap() { return WorkerCap(); }
+
 ActiveEncode::ActiveEncode() { g_active_encodes.fetch_add(1, std::memory_order_relaxed); }
 ActiveEncode::~ActiveEncode() { g_active_encodes.fetch_sub(1, std::memory_order_relaxed); }
 

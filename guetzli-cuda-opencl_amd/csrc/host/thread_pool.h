@@ -16,6 +16,10 @@
 namespace gz {
 
 int HostThreads();
+// Encodes in progress in this process, and the pool workers that may run
+// items at once (HostThreads() - encodes in progress, at least 1).
+int ActiveEncodes();
+int PoolWorkerCap();
 
 // An encode in progress (ProcessJpegData): counted while the object lives.
 class ActiveEncode {

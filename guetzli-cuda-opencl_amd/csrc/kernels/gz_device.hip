@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../runtime/engine.h"
+#include "../host/thread_pool.h"
 #include "gz_math.h"
 
 namespace gz {
@@ -602,8 +603,21 @@ static hipError_t WaitOnStream(hipStream_t s) {
   // 200-500 us of polling, 241-246 with 700-1000 us, at 0.046 / 0.056-0.066 /
   // 0.068-0.071 s of host CPU per frame -- +1-4 % for up to +55 % host CPU,
   // so the default stays the sleeping wait (0).
-  constexpr int kSpinUs = 0;
-  static const int spin_us = getenv("GZ_SPIN_US") ? atoi(getenv("GZ_SPIN_US")) : kSpinUs;
+  //
+  // Adaptive (round 5): with at most two encodes in progress in the process
+  // and CPUs to spare -- one frame alone, a strip rank -- nothing competes
+  // for the host cores and the wait polls for up to kSpinIdleUs first, so a
+  // lone frame's many short waits (the change order, the bulk prefix, each
+  // candidate) end when the work does; with more encodes in flight it
+  // sleeps at once as before (the concurrent bench's CPU per frame is
+  // unchanged).  GZ_SPIN_US >= 0 fixes the polling time for every wait.
+  constexpr int kSpinIdleUs = 5000;
+  static const int env_spin = getenv("GZ_SPIN_US") ? atoi(getenv("GZ_SPIN_US")) : -1;
+  int spin_us = env_spin;
+  if (spin_us < 0) {
+    const int active = ActiveEncodes();
+    spin_us = active <= 2 && HostThreads() - active >= 2 ? kSpinIdleUs : 0;
+  }
   if (spin_us > 0) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
@@ -1327,9 +1341,10 @@ struct OrdLayout {
 };
 }  // namespace
 
-bool Engine::OrderReset() {
+bool Engine::OrderReset(bool* unavailable) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  if (unavailable) *unavailable = false;
   const OrdLayout L(nb_);
   if (!d_ord_) {
     // (all three buffers or none: they are committed together)
@@ -1345,6 +1360,11 @@ bool Engine::OrderReset() {
     if (!ok) {
       if (d) (void)hipFree(d);
       if (h) (void)hipHostFree(h);
+      (void)hipGetLastError();  // (the failed allocation's error is handled here)
+      if (unavailable) {
+        *unavailable = true;
+        return true;
+      }
       return Fail("OrderReset: device allocation failed", 0);
     }
     d_ord_ = d;

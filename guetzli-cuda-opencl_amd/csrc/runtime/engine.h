@@ -202,7 +202,9 @@ class Engine {
   // weight * val_threshold * direction to max_block_error (applied by the
   // next OrderBuild, ahead of its weights).
   bool HasOrderCandidates() const { return ord_cand_n_ >= 0; }
-  bool OrderReset();
+  // (*unavailable: the order's buffers could not be allocated -- the caller
+  // builds the order on the host; false is then not returned for it)
+  bool OrderReset(bool* unavailable = nullptr);
   // (entries: also fill and download the entries in the same synchronisation
   // -- the common case, a radius with entries -- instead of OrderFetch)
   bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,

@@ -30,6 +30,7 @@ __global__ __launch_bounds__(64) void k_occupy(const uint32_t* release, uint32_t
       if (wall_clock64() - t0 > limit_ticks) break;
       __builtin_amdgcn_s_sleep(127);
     }
+    __hip_atomic_fetch_sub(held, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (threadIdx.x == 1) lds[1] = lds[0];
@@ -69,7 +70,8 @@ void* occupy_start(int device, int spare_xcd, int limit_ms) {
   return o;
 }
 
-// Workgroups holding a CU right now (read on a stream of its own).
+// Workgroups holding a CU right now -- started and not yet released or
+// timed out (read on a stream of its own).
 int occupy_held(void* h) {
   Occupy* o = static_cast<Occupy*>(h);
   hipStream_t s;

@@ -196,8 +196,9 @@ def test_coder_forward_progress_under_occupancy(gz, spare_xcd):
     dispatched (jpeg_kernels.inc: look-back fallback + seam counters).
     Another stream's kernel holds every CU but those of one XCD (one
     workgroup with all 160 KiB of LDS per CU); three engines code a 1080p
-    candidate at once while it holds, then the host releases it: every
-    coder finishes with the host writer's bytes."""
+    candidate at once while it holds: every coder finishes while the CUs are
+    still held (only then is the holding kernel released), with the host
+    writer's bytes."""
     import concurrent.futures
     import time
     w, h = 1920, 1080
@@ -218,10 +219,15 @@ def test_coder_forward_progress_under_occupancy(gz, spare_xcd):
         held = L.occupy_held(occ)
         with concurrent.futures.ThreadPoolExecutor(max_workers=3) as ex:
             futs = [ex.submit(c.write_jpeg, co, quant) for c in cmps]
-            time.sleep(0.3)
+            # forward progress: the coders finish on the one free XCD,
+            # with the other CUs still held
+            done, pending = concurrent.futures.wait(futs, timeout=12.0)
+            still_held = L.occupy_held(occ)
             assert L.occupy_release(occ) == 0
             released = True
             outs = [f.result(timeout=60) for f in futs]
+            assert not pending, "%d coders did not finish while the CUs were held" % len(pending)
+            assert still_held >= 160, "the holding kernel let go early (%d CUs)" % still_held
     finally:
         if not released:
             L.occupy_release(occ)
@@ -446,3 +452,38 @@ def test_process_edge_known_answers(gz, name):
     data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
     assert st.iterations == e["iters"]
     assert hashlib.sha256(data).hexdigest() == e["sha256"]
+
+
+_ENV_ENCODE = r"""
+import hashlib, json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import guetzli_amd as gz
+e = json.loads(sys.argv[2])
+rgb = gz.synthetic_frame(e["seed"], e["w"], e["h"])
+data, stats = gz.process(rgb, e["w"], e["h"], gz.Params.for_quality(e["quality"]), return_stats=True)
+d = gz.last_process_detail()
+print(json.dumps({"sha": hashlib.sha256(data).hexdigest(), "iters": stats.iterations,
+                  "undone": d.get("backend_spec_undone", 0), "codes": d.get("backend_entropy_codes", 0)}))
+"""
+
+
+@pytest.mark.parametrize("env", [{"GZ_REPLAY_DIV": "1000000"}, {"GZ_SPEC_DECADES": "1"},
+                                 {"GZ_SPEC_DECADES": "32", "GZ_SPIN_US": "0"}])
+def test_backend_variants_keep_known_answer(env):
+    """Back-end variants that must not change the bytes (each in its own
+    process: the knobs are read once).  GZ_REPLAY_DIV=1e6: every journal
+    counts as long, so each sync after the device bulk prefix replays a
+    journal over a partial host copy (that used to fail the
+    encode); GZ_SPEC_DECADES: the speculative tail's batch fixed at one
+    rebuild (the one-at-a-time loop) or 32."""
+    import subprocess
+    import sys
+    name = "synth_640x360_s3_q95"
+    e = dict(MANIFEST["synthetic"][name])
+    pkg = os.path.join(os.path.dirname(GOLDEN), "..", "guetzli-cuda-opencl_amd", "python")
+    res = subprocess.run([sys.executable, "-c", _ENV_ENCODE, pkg, json.dumps(e)], env=dict(os.environ, **env),
+                         capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["sha"] == e["sha256"] and out["iters"] == e["iters"], out

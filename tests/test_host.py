@@ -193,3 +193,18 @@ def test_process_edge_paths_without_device(gz, name):
     data, st = gz.process(rgb, e["w"], e["h"], p, return_stats=True)
     assert st.iterations == e["iters"] == 0
     assert hashlib.sha256(data).hexdigest() == e["sha256"]
+
+
+@pytest.mark.parametrize("decades", ["1", "3", "32"])
+def test_speculative_tail_batches_bit_exact(host_e2e_bin, decades, tmp_path):
+    """The back end's tail runs in speculative batches (codes of several
+    decades built at once, changes past the break undone); the batch size
+    must not change a byte or an iteration."""
+    e = MANIFEST["e2e"]["bees_q95"]
+    out = tmp_path / "out.jpg"
+    res = subprocess.run([host_e2e_bin, os.path.join(GOLDEN, e["input"]), str(e["w"]), str(e["h"]),
+                          str(e["quality"]), str(out)], capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, GZ_SPEC_DECADES=decades))
+    assert res.returncode == 0, res.stderr
+    assert json.loads(res.stdout)["iters"] == e["iters"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
