@@ -612,21 +612,63 @@ bool HipButteraugliComparator::DeviceOrderReset(bool* available) {
 }
 
 bool HipButteraugliComparator::DeviceChangeOrder(int direction, double target_mul, bool zero_bmax,
-                                                 const std::vector<int>& last_indexes,
-                                                 std::vector<std::pair<int, float>>* order,
-                                                 int* blocks_to_change) {
+                                                 const std::vector<int>& last_indexes, float floor_limit,
+                                                 size_t* n_entries, int* blocks_to_change, int64_t* below_floor) {
   // (ComputeBlockErrorAdjustmentWeights' target distance: target * target_mul
   // in double, butteraugli_comparator.cc:175)
   const double td = target_ * target_mul;
+  *n_entries = 0;
   for (int rblock = 1; rblock <= 4; ++rblock) {
-    size_t n = 0;
-    // (the entries come back with the counts: one wait per radius)
-    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, &n, blocks_to_change, order)) {
+    // (the entries are filled with the counts: one wait per radius)
+    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, n_entries, blocks_to_change,
+                             floor_limit, below_floor)) {
       err_ = engine_->error();
       return false;
     }
-    if (n) break;
+    if (*n_entries) break;
   }
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceOrderEntries(std::vector<std::pair<int, float>>* order) {
+  const auto t0 = Clock::now();
+  order->resize(engine_->OrderEntryCount());
+  if (!engine_->OrderFetch(order->data(), order->size())) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_bulk += Since(t0);
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceSelectBulk(const CoeffImage& img, size_t bulk, size_t window, int direction,
+                                                Engine::OrderSelection* sel, JpegHistogram ac[3]) {
+  const auto t0 = Clock::now();
+  if (bulk && !SyncCoeffs(img)) return false;
+  int32_t delta[3][256];
+  if (!engine_->OrderSelect(bulk, window, direction, img.quant, true, sel, delta)) {
+    err_ = engine_->error();
+    return false;
+  }
+  if (sel->applied) {
+    // (the counts are stored doubled, JpegHistogram::Add)
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < 256; ++i) ac[c].counts[i] += 2u * static_cast<uint32_t>(delta[c][i]);
+  }
+  seconds_bulk += Since(t0);
+  return true;
+}
+
+bool HipButteraugliComparator::DeviceSelectWindow(size_t from, size_t window, int direction,
+                                                  Engine::OrderSelection* sel) {
+  const auto t0 = Clock::now();
+  int32_t delta[3][256];
+  const int q[3][kDCTBlockSize] = {};
+  if (!engine_->OrderSelect(from, window, direction, q, false, sel, delta)) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_bulk += Since(t0);
   return true;
 }
 
@@ -1626,6 +1668,7 @@ class Processor {
   double encode_s_ = 0.0;
   double final_score_ = -1;
   std::vector<int> bulk_cnt_;  // per-block change counts of a back-end bulk prefix
+  size_t tail_len_[2] = {0, 0};  // the last back-end tail's length per direction (up, down)
   StripOrder strip_order;      // (a frame split over ranks)
   static constexpr int kOrderChunk = 1024;     // blocks per parallel back-end work item
   static constexpr size_t kMinBulkChanges = 64;
@@ -1760,9 +1803,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // the frame's candidates and block maxima are resident) unless the frame
   // is split over ranks or the comparator has no device
   bool device_order = false;
-  if (!part_ && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
-  // With the device order the bulk prefix is applied on the device too
-  // (DeviceBulkApply), with the change of the AC histograms counted there.
+  if (!part_ && cmp_->HasDeviceBulk() && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
+  // With the device order the bulk prefix is selected and applied on the
+  // device too (DeviceSelectBulk), with the change of the AC histograms
+  // counted there.
   // The host copy of a block then follows lazily: a block's coefficients are a function of
   // its last_indexes alone -- its first last_indexes[b] candidates zeroed,
   // the others as quantized (up iterations zero candidates in order, down
@@ -1809,9 +1853,13 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       bool strip_exact = part_ && part_->world > 1 && !StripFastOrder();
       const bool strip_fast = part_ && part_->world > 1 && !strip_exact;
       size_t frame_n = 0;
+      int64_t device_below_floor = -1;
       if (device_order) {
-        if (!cmp_->DeviceChangeOrder(direction, target_mul, first_up_iter, last_indexes, &global_order,
-                                     &blocks_to_change))
+        // (the entries stay on the device; the first up iteration's count of
+        // keys below its floor comes back with their count)
+        const float floor_limit = first_up_iter ? 0.75f * cmp_->BlockErrorLimit() : -HUGE_VALF;
+        if (!cmp_->DeviceChangeOrder(direction, target_mul, first_up_iter, last_indexes, floor_limit, &frame_n,
+                                     &blocks_to_change, first_up_iter ? &device_below_floor : nullptr))
           return Fail(err);
       } else if (!first_up_iter && (cmp_->block_max_distance(), cmp_->block_max_failed())) {
         return Fail(err);
@@ -1821,7 +1869,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
                                    &blocks_to_change, strip_fast ? &frame_n : nullptr)) {
         return exchange_failed();
       }
-      if (!strip_fast) frame_n = global_order.size();
+      if (!strip_fast && !device_order) frame_n = global_order.size();
       res_->detail["backend_order_s"] += Since(tb);
       res_->detail["backend_order_entries"] += static_cast<double>(frame_n);
       if (frame_n == 0) {
@@ -1831,7 +1879,17 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // std::sort(global_order) by key (processor.cc:840-843), materialised
       // lazily: only the prefix the change loop consumes gets sorted.
       std::unique_ptr<LazyStdSort> sorter;
-      if (!strip_fast) sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
+      if (!strip_fast && !device_order) sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
+      // device order: the entries come to the host (all of them, in block
+      // order, for std::sort's exact permutation) only where the keys leave
+      // the order open
+      auto fetch_exact = [&]() -> bool {
+        if (!cmp_->DeviceOrderEntries(&global_order)) return false;
+        if (global_order.size() != frame_n) return false;
+        sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
+        res_->detail["backend_order_fetches"] += 1;
+        return true;
+      };
       // strip_fast: this rank's entries, global_order, become the frame's (the
       // exact path) when their keys leave std::sort's order open
       auto go_exact = [&]() -> bool {
@@ -1851,6 +1909,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         for (const auto& e : global_order) below_floor += e.second < limit ? 1 : 0;
         if (!part_->SumAll(&below_floor, 1)) return exchange_failed();
       }
+      if (device_order && first_up_iter) below_floor = device_below_floor;
       ChangeLoop loop(direction, cmp_->DistanceOK(1.0), base_size, 1, blocks_to_change, &first_up_iter,
                       cmp_->BlockErrorLimit(), global_order, frame_n, below_floor);
       int est_jpg_size = prev_size;
@@ -1871,7 +1930,68 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         const long first_read = std::min(std::min(first_code, m), n - 1);
         if (first_read >= kMinBulkChanges) bulk = static_cast<size_t>(first_read);
       }
-      if (bulk) {
+      // The device order's selection: the bulk prefix as a set from the keys
+      // (applied on the device) and the tail's window of the next entries.
+      Engine::OrderSelection sel;
+      std::vector<std::pair<int, float>> win;  // the tail from position win_base on, in order
+      size_t win_base = bulk;
+      size_t win_ok = 0;                       // ... its positions certified to be std::sort's
+      bool win_last = false;                   // ... and it holds every entry left
+      if (device_order) {
+        const auto tbk = Clock::now();
+        // (the window: twice the last tail of this direction, 512 .. 8192
+        // entries -- sorted in one workgroup on the device; GZ_TAIL_WINDOW:
+        // a fixed size, for tests)
+        static const size_t fixed_window = [] {
+          const char* w = std::getenv("GZ_TAIL_WINDOW");
+          return static_cast<size_t>(w && std::atoi(w) > 0 ? std::atoi(w) : 0);
+        }();
+        size_t& last_tail = tail_len_[direction > 0 ? 0 : 1];
+        const size_t kTailWindow =
+            fixed_window ? fixed_window : std::min<size_t>(8192, std::max<size_t>(512, 2 * last_tail));
+        JpegHistogram ac_now[3];
+        for (int c = 0; c < ncomp && c < 3; ++c) ac_now[c] = ac_histograms[c];
+        if (!cmp_->DeviceSelectBulk(*img, bulk, kTailWindow, direction, &sel, ac_now)) return Fail(err);
+        if (bulk && sel.applied) {
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          for (int bix = 0; bix < num_blocks; ++bix) last_indexes[bix] += sel.cnt[bix] * direction;
+          if (sel.tie_block >= 0) last_indexes[sel.tie_block] += sel.take * direction;
+          img->host_partial = true;
+          refresh_raw();
+          loop.changed = static_cast<int>(bulk);
+          res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+          res_->detail["backend_bulk_device"] += 1;
+        } else if (bulk) {
+          // K* shared by several blocks across the prefix's end: std::sort's
+          // tie order decides which of them the prefix takes -- the exact
+          // path (every entry, LazyStdSort), applied with the host's counts
+          res_->detail["backend_select_open"] += 1;
+          if (!fetch_exact()) return Fail(err);
+          sorter->SetPrefix(bulk);
+          bulk_cnt8.assign(num_blocks, 0);
+          for (size_t i = 0; i < bulk; ++i) ++bulk_cnt8[global_order[i].first];
+          for (int bix = 0; bix < num_blocks; ++bix) last_indexes[bix] += bulk_cnt8[bix] * direction;
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_now[c] = ac_histograms[c];
+          if (!cmp_->DeviceBulkApply(*img, direction, bulk_cnt8.data(), ac_now)) return Fail(err);
+          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          img->host_partial = true;
+          refresh_raw();
+          loop.changed = static_cast<int>(bulk);
+          res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+          res_->detail["backend_bulk_device"] += 1;
+        }
+        if (!sorter && !sel.window_overflow) {
+          // the window, sorted on the device: std::sort's order for its first
+          // window_ok positions (up to the first key shared by entries of
+          // several blocks; entries of one block are interchangeable: a
+          // change takes the block's next candidate)
+          win.swap(sel.window);
+          win_ok = sel.window_ok;
+          win_last = sel.window_last;
+        }
+        res_->detail["backend_bulk_s"] += Since(tbk);
+      }
+      if (bulk && !device_order) {
         const auto tbk = Clock::now();
         if (strip_fast) {
           // the prefix as a set from the keys alone (StripOrder::Prefix);
@@ -1895,38 +2015,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           });
         }
-        if (device_bulk) {
-          // the changes on the device and a recount of the AC histograms
-          // there; the host only advances last_indexes (blocks materialise
-          // lazily)
-          bulk_cnt8.resize(num_blocks);
-          // (a few ns per block: on the pool only for very large frames)
-          const int slices = own_hi - own_lo >= (1 << 19) ? 16 : 1;
-          ParallelFor(slices, [&](int sl) {
-            const int b0 = own_lo + static_cast<int>(static_cast<int64_t>(own_hi - own_lo) * sl / slices);
-            const int b1 = own_lo + static_cast<int>(static_cast<int64_t>(own_hi - own_lo) * (sl + 1) / slices);
-            for (int bix = b0; bix < b1; ++bix) {
-              bulk_cnt8[bix] = static_cast<uint8_t>(bulk_cnt_[bix]);
-              last_indexes[bix] += bulk_cnt_[bix] * direction;
-            }
-          });
-          JpegHistogram ac_now[3];
-          for (int c = 0; c < ncomp && c < 3; ++c) ac_now[c] = ac_histograms[c];
-          if (!cmp_->DeviceBulkApply(*img, direction, bulk_cnt8.data(), ac_now)) return Fail(err);
-          for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
-          img->host_partial = true;
-          refresh_raw();
-          loop.changed = static_cast<int>(bulk);
-          res_->detail["backend_bulk_s"] += Since(tbk);
-          res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
-          res_->detail["backend_bulk_device"] += 1;
-        }
         struct ChunkDelta {
           JpegHistogram h[3];
           std::vector<uint32_t> changed;
         };
-        std::vector<ChunkDelta> deltas(device_bulk ? 0 : own_chunks);
-        if (!device_bulk) ParallelFor(own_chunks, [&](int ch) {
+        std::vector<ChunkDelta> deltas(own_chunks);
+        ParallelFor(own_chunks, [&](int ch) {
           ChunkDelta& d = deltas[ch];
           int64_t raw_unused = 0;
           const int b0 = own_lo + ch * kOrderChunk, b1 = std::min(own_hi, b0 + kOrderChunk);
@@ -1987,7 +2081,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             last_indexes[bix] = li;
           }
         });
-        if (!device_bulk) {
+        {
         // (symbols only: the last slot is the histogram's fixed sentinel count)
         std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1), 0);
         for (const ChunkDelta& d : deltas) {
@@ -2059,20 +2153,56 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         // misses of a chunk overlap instead of chaining.  Values are only
         // prefetched; the loop below reads them as before.
         size_t prefetched = bulk;
+        // The tail's entries: the device window's certified positions, else
+        // (past them, or without a window) std::sort's exact order -- all
+        // entries fetched once, LazyStdSort with the prefix set aside; the
+        // window's positions before are the same in it (see above)
+        bool tail_exact = !device_order || static_cast<bool>(sorter);
+        auto tail_block = [&](size_t s) { return tail_exact ? global_order[s].first : win[s - win_base].first; };
+        auto tail_key = [&](size_t s) { return tail_exact ? global_order[s].second : win[s - win_base].second; };
+        auto tail_ready = [&](size_t s) -> bool {
+          if (!tail_exact) {
+            if (s < win_base + win_ok) return true;
+            if (win_ok == win.size() && !win_last && s == win_base + win_ok) {
+              // the window ran out without a tie: the next one from rank s
+              Engine::OrderSelection next;
+              const size_t want = std::min<size_t>(8192, 2 * win.size());
+              if (!cmp_->DeviceSelectWindow(s, want, direction, &next)) return false;
+              res_->detail["backend_tail_windows"] += 1;
+              if (!next.open && !next.window_overflow) {
+                win.swap(next.window);
+                win_base = s;
+                win_ok = next.window_ok;
+                win_last = next.window_last;
+                if (s < win_base + win_ok) return true;
+              }
+            }
+            if (!fetch_exact()) return false;
+            if (bulk) sorter->SetPrefix(bulk);
+            tail_exact = true;
+            res_->detail["backend_tail_exact"] += 1;
+          }
+          if (s >= sorter->sorted()) {
+            const auto ts = Clock::now();
+            sorter->EnsureSorted(s);
+            sort_s += Since(ts);
+          }
+          return true;
+        };
         auto prefetch_chunk = [&](size_t lo, size_t hi) {
           for (size_t j = lo; j < hi; ++j) {
-            const int b = global_order[j].first;
+            const int b = tail_block(j);
             __builtin_prefetch(&last_indexes[b]);
             __builtin_prefetch(&offsets[b]);
           }
           for (size_t j = lo; j < hi; ++j) {
-            const int b = global_order[j].first;
+            const int b = tail_block(j);
             const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
             const int ci = off + last_indexes[b] + std::min(direction, 0);
             if (ci >= 0 && ci < static_cast<int>(cand.size())) __builtin_prefetch(&cand[ci]);
           }
           for (size_t j = lo; j < hi; ++j) {
-            const int b = global_order[j].first;
+            const int b = tail_block(j);
             const int off = std::max(0, std::min(offsets[b], static_cast<int>(cand.size()) - 1));
             const int ci = off + last_indexes[b] + std::min(direction, 0);
             if (ci < 0 || ci >= static_cast<int>(cand.size())) continue;
@@ -2123,26 +2253,27 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           size_t ns = 0;
           // A: the batch's changes, their symbol updates into the histograms
           for (size_t s = i; s < j; ++s) {
-            if (s >= sorter->sorted()) {
-              const auto ts = Clock::now();
-              sorter->EnsureSorted(s);
-              sort_s += Since(ts);
-            }
+            if (!tail_ready(s)) return Fail(err);
             if (s >= prefetched) {
-              prefetched = std::max(sorter->sorted(), s + 1);
+              prefetched = tail_exact ? std::max(sorter->sorted(), s + 1) : std::min(win_base + win_ok, s + 256);
               prefetch_chunk(s, std::min(prefetched, n_order));
             }
-            const int bix = global_order[s].first;
+            const int bix = tail_block(s);
             if (device_bulk) materialize(bix);
             const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
-            const int idx = cand[off + last_indexes[bix] + std::min(direction, 0)];
+            const int li = last_indexes[bix] + std::min(direction, 0);
+            if (li < 0 || off + li >= offsets[bix + 1]) {  // (an order entry without a candidate: a bug)
+              if (err) *err = "back end: change order names a block without candidates left";
+              return false;
+            }
+            const int idx = cand[off + li];
             Spec sp;
             sp.bix = bix;
             sp.c = idx / kDCTBlockSize;
             sp.k = idx % kDCTBlockSize;
             sp.old = img->block(sp.c, bix)[sp.k];
             sp.nz = acm.nz[static_cast<size_t>(sp.c) * num_blocks + bix];
-            sp.key = global_order[s].second;
+            sp.key = tail_key(s);
             apply(bix, &sp.log);
             for (int e = 0; e < sp.log.n; ++e) ac_histograms[sp.c].Add(sp.log.sym[e], sp.log.weight[e]);
             spec.push_back(sp);
@@ -2332,6 +2463,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           window *= 2;
         }
       }
+      if (device_order) tail_len_[direction > 0 ? 0 : 1] = static_cast<size_t>(loop.changed) - bulk;
       res_->detail["backend_changes_s"] += Since(tc);
       res_->detail["backend_codes_s"] += codes_s;
       res_->detail["backend_sort_s"] += sort_s;

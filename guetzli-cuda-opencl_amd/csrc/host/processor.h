@@ -107,7 +107,12 @@ class Comparator {
   // device): DeviceOrderReset before an iteration loop (max_block_error :=
   // 0), DeviceChangeOrder per iteration (the weights at radius 1..4 until
   // some block has entries; the entries in block order, as
-  // Processor::BuildChangeOrder makes them), DeviceOrderAdvance after it.
+  // Processor::BuildChangeOrder makes them, stay on the device: their count
+  // and the blocks with entries come back, and with floor_limit > -inf the
+  // count of keys below it), DeviceSelectBulk (the bulk prefix selected and
+  // applied there, and the tail's window), DeviceOrderEntries (every entry,
+  // for std::sort's exact order where the keys leave it open),
+  // DeviceOrderAdvance after the iteration.
   // DeviceOrderReset: false on an engine error (error() says which);
   // *available = false: no device order, build on the host.
   virtual bool DeviceOrderReset(bool* available) {
@@ -115,8 +120,21 @@ class Comparator {
     return true;
   }
   virtual bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax,
-                                 const std::vector<int>& last_indexes,
-                                 std::vector<std::pair<int, float>>* order, int* blocks_to_change) {
+                                 const std::vector<int>& last_indexes, float floor_limit, size_t* n_entries,
+                                 int* blocks_to_change, int64_t* below_floor) {
+    return false;
+  }
+  virtual bool DeviceOrderEntries(std::vector<std::pair<int, float>>* order) { return false; }
+  // The first `bulk` entries of std::sort's order as a set, selected and
+  // applied on the device (Engine::OrderSelect: nothing applied when sel->open),
+  // ac updated as DeviceBulkApply does, and the tail's window of entries.
+  virtual bool DeviceSelectBulk(const CoeffImage& img, size_t bulk, size_t window, int direction,
+                                Engine::OrderSelection* sel, JpegHistogram ac[3]) {
+    return false;
+  }
+  // The tail's next window: the entries after the first `from` of std::sort's
+  // order (as a set), selected on the device as DeviceSelectBulk's window is.
+  virtual bool DeviceSelectWindow(size_t from, size_t window, int direction, Engine::OrderSelection* sel) {
     return false;
   }
   virtual bool DeviceOrderAdvance(float val_threshold, int direction) { return false; }
@@ -248,7 +266,11 @@ class HipButteraugliComparator : public Comparator {
   const std::string& error() const override { return err_; }
   bool DeviceOrderReset(bool* available) override;
   bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
-                         std::vector<std::pair<int, float>>* order, int* blocks_to_change) override;
+                         float floor_limit, size_t* n_entries, int* blocks_to_change, int64_t* below_floor) override;
+  bool DeviceOrderEntries(std::vector<std::pair<int, float>>* order) override;
+  bool DeviceSelectBulk(const CoeffImage& img, size_t bulk, size_t window, int direction,
+                        Engine::OrderSelection* sel, JpegHistogram ac[3]) override;
+  bool DeviceSelectWindow(size_t from, size_t window, int direction, Engine::OrderSelection* sel) override;
   bool DeviceOrderAdvance(float val_threshold, int direction) override;
   bool HasDeviceBulk() const override { return true; }
   bool HasKnownHistogramEncode() const override { return true; }

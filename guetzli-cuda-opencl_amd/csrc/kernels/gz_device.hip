@@ -34,8 +34,8 @@ __constant__ GzTables c_tab;
 #include "block_zeroing.inc"
 #include "block_zeroing420.inc"
 #include "coeff_kernels.inc"
-#include "jpeg_kernels.inc"
 #include "order_kernels.inc"
+#include "jpeg_kernels.inc"
 
 namespace gz {
 
@@ -671,6 +671,9 @@ Engine::~Engine() {
   if (h_delta_val_) hipHostFree(h_delta_val_);
   if (h_ord_) hipHostFree(h_ord_);
   if (h_ord_entries_) hipHostFree(h_ord_entries_);
+  if (h_win_) hipHostFree(h_win_);
+  if (d_win_) hipFree(d_win_);
+  if (d_ord_entries_) hipFree(d_ord_entries_);
   if (h_cbreq_) (void)hipHostFree(h_cbreq_);
   if (stream_) hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
@@ -1317,13 +1320,15 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 }
 
 // ---- the back end's change order (order_kernels.inc) ----
-// Host <-> device traffic through mapped pinned memory (no copy launches):
-// the kernels read last_indexes (bytes) from h_ord_ and write the totals after it
-// and the entries into h_ord_entries_; the host reads them after the
-// stream synchronisation.
+// The kernels read last_indexes (bytes) from the mapped pinned h_ord_ and
+// write the totals after it; the entries stay in HBM (d_ord_entries_), where
+// the selection of the bulk prefix and of the tail window reads them
+// (OrderSelect); only the window, the per-block prefix counts and the
+// selection's result cross to the host (mapped), or all entries when the
+// host takes the exact path (OrderFetch).
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, info, arr, mbe, last, first, part, bytes;
+  size_t weight, active, cnt, off, info, arr, mbe, last, first, part, sel, cnt8, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
@@ -1336,9 +1341,14 @@ struct OrdLayout {
     last = mbe + a;
     first = last + a;  // the fill's tile starts: (entries <= 193 n) / 256 + 1 <= n + 4
     part = first + ((n + 4) * 4 + 255) / 256 * 256;  // 2 ints per counting workgroup
-    bytes = part + ((n / 256 + 2) * 8 + 255) / 256 * 256;
+    sel = part + ((n / 256 + 2) * 8 + 255) / 256 * 256;  // the selection's counts and state
+    cnt8 = sel + (SelLayout::words * 4 + 255) / 256 * 256;  // per-block prefix counts (bytes)
+    bytes = cnt8 + (n + 255) / 256 * 256;
   }
 };
+// mapped pinned h_ord_: last_indexes [nb] bytes | totals [8] | below_floor | SelHost
+constexpr int kOrdInfoInts = 8;
+size_t OrdHostBytes(int nb) { return static_cast<size_t>(nb) * 4 + 64 + sizeof(SelHost) + 64; }
 }  // namespace
 
 bool Engine::OrderReset(bool* unavailable) {
@@ -1353,10 +1363,10 @@ bool Engine::OrderReset(bool* unavailable) {
     int* m = nullptr;
     const bool ok =
         hipMalloc(&d, L.bytes) == hipSuccess &&
-        hipHostMalloc(reinterpret_cast<void**>(&h), static_cast<size_t>(nb_) * 4 + 64, hipHostMallocCoherent) ==
-            hipSuccess &&
+        hipHostMalloc(reinterpret_cast<void**>(&h), OrdHostBytes(nb_), hipHostMallocCoherent) == hipSuccess &&
         hipHostGetDevicePointer(reinterpret_cast<void**>(&m), h, 0) == hipSuccess &&
-        hipMemsetAsync(static_cast<char*>(d) + L.info, 0, L.mbe - L.info, s) == hipSuccess;  // totals, arrivals
+        hipMemsetAsync(static_cast<char*>(d) + L.info, 0, L.mbe - L.info, s) == hipSuccess &&  // totals, arrivals
+        hipMemsetAsync(static_cast<char*>(d) + L.sel, 0, L.cnt8 - L.sel, s) == hipSuccess;  // (its arrivals)
     if (!ok) {
       if (d) (void)hipFree(d);
       if (h) (void)hipHostFree(h);
@@ -1374,25 +1384,40 @@ bool Engine::OrderReset(bool* unavailable) {
   }
   GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
   ord_adv_dir_ = 0;
+  ord_n_ = 0;
+  return true;
+}
+
+bool Engine::OrderEntriesCapacity(size_t n) {
+  const size_t bytes = n * sizeof(OrderEntry);
+  if (bytes > d_ord_entries_cap_) {
+    if (d_ord_entries_) GZ_HIP(hipFree(d_ord_entries_));
+    d_ord_entries_ = nullptr;
+    d_ord_entries_cap_ = 0;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    GZ_HIP(hipMalloc(&d_ord_entries_, cap));
+    d_ord_entries_cap_ = cap;
+  }
   return true;
 }
 
 bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
                         const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change,
-                        std::vector<std::pair<int, float>>* entries) {
+                        float floor_limit, int64_t* below_floor) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderBuild without candidates", 0);
-  // (the fused fill writes at most cand_n + nb entries: the mapped buffer
-  // holds that many before anything is queued)
+  // (the fill writes at most cand_n + nb entries: the buffer holds that many
+  // before anything is queued)
   const size_t max_entries = static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_);
-  if (entries && !OrderEntriesCapacity(max_entries)) return false;
+  if (!OrderEntriesCapacity(max_entries)) return false;
   if (static_cast<int>(last_indexes.size()) != nb_ || rblock < 1 || rblock > 4)
     return Fail("OrderBuild arguments", 0);
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
   float* weight = reinterpret_cast<float*>(base + L.weight);
   int* active = reinterpret_cast<int*>(base + L.active);
+  uint32_t* sel = reinterpret_cast<uint32_t*>(base + L.sel);
   const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, direction,
                     reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.part),
                     reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
@@ -1418,43 +1443,32 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   GZ_TIMED("order_build", k_order_local<<<groups, 256, 0, s>>>(d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock,
                                                                 target_distance, weight, active,
                                                                 reinterpret_cast<float*>(base + L.mbe),
-                                                                ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, a));
+                                                                ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, sel,
+                                                                SelLayout::words, a));
   if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
   ord_direction_ = direction;
-  // with `entries`: the offsets and the entries queued behind the counts
-  // (the fill reads the total from the offsets; a grid for the largest
-  // possible count, its workgroups past the total leave at once), one wait
-  if (entries && !OrderFillEnqueue(max_entries)) return false;
+  // the offsets and the entries queued behind the counts (the fill reads
+  // the total from the offsets; a grid for the largest possible count, its
+  // workgroups past the total leave at once), one wait
+  if (!OrderFillEnqueue(max_entries, floor_limit)) return false;
+  int* host_floor = h_ord_ + nb_ + kOrdInfoInts;
+  if (below_floor) {
+    GZ_HIP(hipMemcpyAsync(host_floor, sel + SelLayout::state + offsetof(SelState, below_floor) / 4, 4,
+                          hipMemcpyDeviceToHost, s));
+  }
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
   *blocks_to_change = h_ord_[nb_ + rblock - 1];
   *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
-  if (entries) {
-    // (one pass: no value-initialisation of the vector before the copy)
-    static_assert(sizeof(OrderEntry) == sizeof(std::pair<int, float>), "entry layout");
-    const auto* src = static_cast<const std::pair<int, float>*>(h_ord_entries_);
-    entries->assign(src, src + *n_entries);
-  }
-  return true;
-}
-
-bool Engine::OrderEntriesCapacity(size_t n) {
-  const size_t bytes = n * sizeof(OrderEntry);
-  if (bytes > h_ord_entries_cap_) {
-    if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
-    h_ord_entries_ = nullptr;
-    h_ord_entries_cap_ = 0;
-    const size_t cap = bytes + bytes / 4 + 4096;
-    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap, hipHostMallocCoherent));
-    GZ_HIP(hipHostGetDevicePointer(&m_ord_entries_, h_ord_entries_, 0));
-    h_ord_entries_cap_ = cap;
-  }
+  if (below_floor) *below_floor = *host_floor;
+  ord_n_ = *n_entries;
+  ord_selects_ = 0;
   return true;
 }
 
 // the scan of this build's counts and the fill of up to `grid_entries`
-// entries (the fill takes the true total from the scan)
-bool Engine::OrderFillEnqueue(size_t grid_entries) {
+// entries into HBM (the fill takes the true total from the scan)
+bool Engine::OrderFillEnqueue(size_t grid_entries, float floor_limit) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
@@ -1470,7 +1484,8 @@ bool Engine::OrderFillEnqueue(size_t grid_entries) {
   if (grid_entries == 0) return true;
   GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((grid_entries + 255) / 256), 256, 0, s>>>(
       reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
-      off, first, static_cast<OrderEntry*>(m_ord_entries_), a));
+      off, first, static_cast<OrderEntry*>(d_ord_entries_), reinterpret_cast<uint32_t*>(base + L.sel), floor_limit,
+      a));
   return true;
 }
 
@@ -1479,37 +1494,42 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (!n) return true;
-  // (at most cand_n + nb: a block past the last candidate reads one, the
-  // host's clamp of its offset into [0, cand_n - 1])
-  if (n > static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_)) return Fail("OrderFetch entry count", 0);
-  if (!OrderEntriesCapacity(n) || !OrderFillEnqueue(n)) return false;
-  GZ_HIP(WaitOnStream(s));
+  if (n != ord_n_) return Fail("OrderFetch entry count", 0);
+  const size_t bytes = n * sizeof(OrderEntry);
+  if (bytes > h_ord_entries_cap_) {
+    if (h_ord_entries_) GZ_HIP(hipHostFree(h_ord_entries_));
+    h_ord_entries_ = nullptr;
+    h_ord_entries_cap_ = 0;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    GZ_HIP(hipHostMalloc(&h_ord_entries_, cap));
+    h_ord_entries_cap_ = cap;
+  }
+  GZ_HIP(hipMemcpyAsync(h_ord_entries_, d_ord_entries_, bytes, hipMemcpyDeviceToHost, s));
+  GZ_HIP(WaitIdle(s));
   ProfFlush();
-  memcpy(static_cast<void*>(out), h_ord_entries_, n * sizeof(OrderEntry));
+  memcpy(static_cast<void*>(out), h_ord_entries_, bytes);
   return true;
 }
 
-bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]) {
-  hipStream_t s = static_cast<hipStream_t>(stream_);
-  GZ_HIP(hipSetDevice(device_));
-  if (ord_cand_n_ < 0 || !d_ord_) return Fail("BulkApply without a change order", 0);
-  if (!h_bulk_) {
-    void* h = nullptr;
-    void* m = nullptr;
-    if (hipHostMalloc(&h, static_cast<size_t>(nb_) + 64, hipHostMallocCoherent) != hipSuccess) {
-      return Fail("BulkApply: pinned allocation failed", 0);
-    }
-    if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) {
-      (void)hipHostFree(h);
-      return Fail("BulkApply: mapped address", 0);
-    }
-    h_bulk_ = static_cast<uint8_t*>(h);
-    m_bulk_ = static_cast<uint8_t*>(m);
-    bytes_ += static_cast<size_t>(nb_) + 64;
+bool Engine::BulkCountsStaging() {
+  if (h_bulk_) return true;
+  void* h = nullptr;
+  void* m = nullptr;
+  if (hipHostMalloc(&h, static_cast<size_t>(nb_) + 64, hipHostMallocCoherent) != hipSuccess) {
+    return Fail("BulkApply: pinned allocation failed", 0);
   }
-  // (the previous BulkApply's kernel, which read the staging, has completed:
-  // its histograms were waited for)
-  memcpy(h_bulk_, cnt, static_cast<size_t>(nb_));
+  if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return Fail("BulkApply: mapped address", 0);
+  }
+  h_bulk_ = static_cast<uint8_t*>(h);
+  m_bulk_ = static_cast<uint8_t*>(m);
+  bytes_ += static_cast<size_t>(nb_) + 64;
+  return true;
+}
+
+bool Engine::BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
   const OrdLayout L(nb_);
   QuantMatrix qm;
   memcpy(qm.q, quant, sizeof(qm.q));
@@ -1521,13 +1541,102 @@ bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt
   const unsigned groups = static_cast<unsigned>(
       std::min(stage_groups, (static_cast<size_t>(nb_) + kBulkWaves - 1) / kBulkWaves));
   GZ_TIMED("bulk_apply", k_bulk_apply<<<groups, kBulkThreads, 0, s>>>(
-      m_bulk_, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
-      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_));
+      cnt_dev, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
+      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_, sel));
+  return true;
+}
+
+bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (ord_cand_n_ < 0 || !d_ord_) return Fail("BulkApply without a change order", 0);
+  if (!BulkCountsStaging()) return false;
+  // (the previous BulkApply's kernel, which read the staging, has completed:
+  // its histograms were waited for)
+  memcpy(h_bulk_, cnt, static_cast<size_t>(nb_));
+  if (!BulkApplyEnqueue(direction, quant, m_bulk_, nullptr)) return false;
   // (a sleeping wait: nothing else of this frame is queued behind it)
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
   for (int c = 0; c < 3; ++c)
     for (int i = 0; i < 256; ++i) delta[c][i] = static_cast<int32_t>(h_jhist_[(2 * c + 1) * 256 + i]);
+  return true;
+}
+
+bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int quant[3][64], bool apply,
+                         OrderSelection* out, int32_t delta[3][256]) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderSelect without a change order", 0);
+  const size_t n = ord_n_;
+  if (n == 0 || bulk >= n || window == 0) return Fail("OrderSelect arguments", 0);
+  if (!BulkCountsStaging()) return false;
+  // (the window is sorted in one workgroup's LDS: at most kSelWindowCap
+  // entries, ties at its keys included; more and the host takes the exact
+  // path)
+  window = std::min<size_t>(window, kSelWindowCap / 2);
+  const size_t cap = kSelWindowCap;
+  if (!h_win_) {
+    GZ_HIP(hipHostMalloc(&h_win_, cap * sizeof(OrderEntry), hipHostMallocCoherent));
+    GZ_HIP(hipHostGetDevicePointer(&m_win_, h_win_, 0));
+    GZ_HIP(hipMalloc(&d_win_, cap * sizeof(OrderEntry)));
+    bytes_ += cap * sizeof(OrderEntry);
+  }
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  uint32_t* sel = reinterpret_cast<uint32_t*>(base + L.sel);
+  uint8_t* cnt8 = reinterpret_cast<uint8_t*>(base + L.cnt8);
+  const OrderEntry* e = static_cast<const OrderEntry*>(d_ord_entries_);
+  const int has_prefix = bulk > 0 ? 1 : 0;
+  const long long ta = static_cast<long long>(bulk) - 1;
+  const long long tb = static_cast<long long>(std::min(n - 1, bulk + window - 1));
+  SelHost* host = reinterpret_cast<SelHost*>(h_ord_ + nb_ + kOrdInfoInts + 16);
+  SelHost* mhost = reinterpret_cast<SelHost*>(m_ord_ + nb_ + kOrdInfoInts + 16);
+  host->done = 0;
+  // (GZ_SELECT_OPEN=1: every prefix reported open -- tests of the exact path)
+  static const int force_open = getenv("GZ_SELECT_OPEN") ? atoi(getenv("GZ_SELECT_OPEN")) : 0;
+  const unsigned rgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(512, (n + 4095) / 4096)));
+  const unsigned cgroups = static_cast<unsigned>(std::min<size_t>((nb_ + 255) / 256, 64 * 71));
+  // (a later selection over the same build -- the tail's next window --
+  // counts rounds 2 and 3 afresh: round 1's counts are the build's)
+  if (ord_selects_++ > 0)
+    GZ_HIP(hipMemsetAsync(sel + SelLayout::h2, 0, (SelLayout::state - SelLayout::h2) * 4, s));
+  GZ_TIMED("order_select",
+           (k_sel_round<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), 2, has_prefix, ta, tb, sel),
+            k_sel_round<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), 3, has_prefix, ta, tb, sel),
+            k_sel_classify<<<cgroups, 256, 0, s>>>(e, reinterpret_cast<const int*>(base + L.off), nb_, has_prefix,
+                                                   static_cast<long long>(bulk), ta, tb, sel, cnt8, m_bulk_,
+                                                   static_cast<OrderEntry*>(d_win_), static_cast<int>(cap),
+                                                   mhost, force_open),
+            k_sel_window_sort<<<1, kSelSortThreads, 0, s>>>(static_cast<const OrderEntry*>(d_win_), sel, has_prefix,
+                                                             static_cast<OrderEntry*>(m_win_), mhost)));
+  if (has_prefix && apply && !BulkApplyEnqueue(direction, quant, cnt8, sel)) return false;
+  GZ_HIP(WaitOnStream(s));
+  ProfFlush();
+  if (!host->done) return Fail("OrderSelect: no result", 0);
+  out->kbits[0] = host->kbits[0];
+  out->kbits[1] = host->kbits[1];
+  out->below = host->below[0];
+  out->eq = host->eq[0];
+  out->straddle = host->straddle != 0;
+  out->take = host->take;
+  out->tie_block = host->straddle ? host->tie_min : -1;
+  out->open = host->open != 0;
+  out->applied = has_prefix && apply && !out->open;
+  out->window_n = static_cast<size_t>(host->win_n);
+  out->window_overflow = out->window_n > cap;
+  out->window_last = static_cast<size_t>(tb) + 1 >= n;
+  out->cnt.assign(h_bulk_, h_bulk_ + nb_);
+  out->window.clear();
+  out->window_ok = 0;
+  if (!out->window_overflow) {
+    const auto* src = static_cast<const std::pair<int, float>*>(h_win_);
+    out->window.assign(src, src + host->win_out);
+    out->window_ok = static_cast<size_t>(host->win_ok);
+  }
+  if (out->applied)
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < 256; ++i) delta[c][i] = static_cast<int32_t>(h_jhist_[(2 * c + 1) * 256 + i]);
   return true;
 }
 

@@ -205,11 +205,14 @@ class Engine {
   // (*unavailable: the order's buffers could not be allocated -- the caller
   // builds the order on the host; false is then not returned for it)
   bool OrderReset(bool* unavailable = nullptr);
-  // (entries: also fill and download the entries in the same synchronisation
-  // -- the common case, a radius with entries -- instead of OrderFetch)
+  // OrderBuild: the entries of the radius are filled into HBM in block order
+  // (with the selection's first counts); floor_limit > -inf: *below_floor =
+  // the entries keyed below it (the first up iteration's floor).
   bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
                   const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change,
-                  std::vector<std::pair<int, float>>* entries = nullptr);
+                  float floor_limit = -__builtin_inff(), int64_t* below_floor = nullptr);
+  size_t OrderEntryCount() const { return ord_n_; }
+  // the n entries (block, key) of the last OrderBuild, in block order
   bool OrderFetch(std::pair<int, float>* out, size_t n);
   bool OrderAdvance(float val_threshold, int direction);
   // The back end's bulk prefix applied to the device copy (k_bulk_apply):
@@ -218,6 +221,35 @@ class Engine {
   // and the change of every component's AC symbol counts it makes
   // (delta[c][symbol], unscaled), waited for.
   bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]);
+  // The first `bulk` entries of the last OrderBuild's std::sort order as a
+  // set, selected on the device by their keys (radix selection of the key
+  // of rank bulk - 1, K*), applied there (k_bulk_apply) -- unless K* is
+  // shared by entries of several blocks across the prefix's end (open: the
+  // keys leave the set to std::sort's tie order, nothing is applied) -- and
+  // the tail's window: every entry keyed from K* up to the key of rank
+  // bulk + window - 1 (K2), in no order, the prefix's K*-keyed entries
+  // among them.  bulk 0: no prefix, the window from the smallest key.
+  struct OrderSelection {
+    uint32_t kbits[2] = {0, 0};  // K*, K2 (StripOrder::Bits order)
+    int below = 0, eq = 0;       // entries keyed below K*, at K*
+    bool straddle = false;       // the prefix takes only `take` of the K*-keyed entries ...
+    int take = 0;
+    int tie_block = -1;          // ... all of tie_block's (when not open)
+    bool open = false;
+    bool applied = false;        // the prefix was applied (cnt: per block, tie_block's take not included)
+    std::vector<uint8_t> cnt;
+    size_t window_n = 0;
+    bool window_overflow = false;  // more than the staging holds: window empty
+    bool window_last = false;      // K2 is the largest key: the window holds every entry left
+    // the tail from position bulk on, in order (the prefix's entries
+    // dropped); its first window_ok positions are std::sort's
+    std::vector<std::pair<int, float>> window;
+    size_t window_ok = 0;
+  };
+  // (apply false: the selection and the window only -- a later window of
+  // the tail, from rank `bulk` on)
+  bool OrderSelect(size_t bulk, size_t window, int direction, const int quant[3][64], bool apply,
+                   OrderSelection* out, int32_t delta[3][256]);
 
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
@@ -228,7 +260,9 @@ class Engine {
   bool OrderEntriesCapacity(size_t n);
   char* RequestStaging(size_t need, char** mapped);  // CompareBlocks* mapped staging
   bool AwaitPosted(const char* h, double* err);
-  bool OrderFillEnqueue(size_t grid_entries);
+  bool OrderFillEnqueue(size_t grid_entries, float floor_limit);
+  bool BulkCountsStaging();
+  bool BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel);
   bool Fail(const char* what, int code);
   void ProfBegin(const char* name);
   void ProfEnd();
@@ -336,9 +370,15 @@ class Engine {
   void* d_ord_ = nullptr;
   int* h_ord_ = nullptr;            // mapped pinned: last_indexes [nb] | totals [8]
   int* m_ord_ = nullptr;            //   (its device address)
-  void* h_ord_entries_ = nullptr;   // mapped pinned: the entries
-  void* m_ord_entries_ = nullptr;
+  size_t ord_n_ = 0;                // entries of the last OrderBuild
+  int ord_selects_ = 0;             // OrderSelect calls since it
+  void* d_ord_entries_ = nullptr;   // the entries (HBM)
+  size_t d_ord_entries_cap_ = 0;
+  void* h_ord_entries_ = nullptr;   // pinned: OrderFetch's staging
   size_t h_ord_entries_cap_ = 0;
+  void* h_win_ = nullptr;           // mapped pinned: OrderSelect's window, in order
+  void* m_win_ = nullptr;
+  void* d_win_ = nullptr;           // ... compacted, in no order (HBM)
   uint8_t* h_bulk_ = nullptr;       // mapped pinned: BulkApply's per-block change counts
   uint8_t* m_bulk_ = nullptr;
 };
