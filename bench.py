@@ -339,7 +339,7 @@ def known_answers(w, h, q):
         return {}
     out = {}
     for e in m.get("synthetic", {}).values():
-        if (e["w"], e["h"], e["quality"]) == (w, h, q):
+        if (e["w"], e["h"], e["quality"]) == (w, h, q) and not e.get("mode"):
             out[e["seed"]] = (e["sha256"], e["iters"])
     return out
 
@@ -385,19 +385,19 @@ def cpu_baseline(width, height, quality, processes=8):
                 reference_bytes_match_manifest="%d/%d" % (matched, cores))
 
 
-def large_frame(gz, dist, world, rank, dev):
+def large_frame(gz, dist, world, rank, dev, w=8192, h=8192, q=84, seed=0):
     """BASELINE configs[4] after the timed region: one synthetic 8192x8192
     frame at q=84 (seed 0, whose reference bytes are committed).  With N >= 4
     GPUs it is split into 4 row strips with a halo over ranks 0-3 (their own
     GPUs, RCCL all-gathers over xGMI: host/strips.h), else encoded by one
     engine.  One untimed encode first (engine creation), then one timed;
-    wall time is the max over the participating ranks; bytes checked."""
+    wall time is the max over the participating ranks; bytes checked.
+    (w, h, q, seed: a smaller known-answer frame -- tests/test_strips.py runs
+    this leg on one GPU with 4 gloo ranks.)"""
     import hashlib
     import torch
-    w = h = 8192
-    q = 84
-    kn = known_answers(w, h, q).get(0)
-    rgb = gz.synthetic_frame(0, w, h)
+    kn = known_answers(w, h, q).get(seed)
+    rgb = gz.synthetic_frame(seed, w, h)
     params = gz.Params.for_quality(q)
     strips = world >= 4
     group = None
@@ -426,7 +426,7 @@ def large_frame(gz, dist, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         elapsed = float(t.item())
     sha = hashlib.sha256(data).hexdigest()
-    return {"config": "BASELINE configs[4]: synthetic 8192x8192 q84 (seed 0)",
+    return {"config": "BASELINE configs[4]: synthetic %dx%d q%d (seed %d)" % (w, h, q, seed),
             "mode": "4 row strips + halo over GPUs 0-3 (RCCL)" if strips else "one engine, 1 GPU",
             "gpus": 4 if strips else 1, "seconds": round(elapsed, 3),
             "Mpixels_per_s": round(w * h / elapsed / 1e6, 3), "bytes": len(data),

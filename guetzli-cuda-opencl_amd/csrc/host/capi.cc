@@ -19,6 +19,7 @@
 #include "host/png_reader.h"
 #include "host/jpeg_writer.h"
 #include "host/processor.h"
+#include "host/rccl_collectives.h"
 #include "host/strips.h"
 #include "host/synthetic.h"
 #include "runtime/engine.h"
@@ -616,5 +617,31 @@ gz_status gz_collectives_selftest(const gz_collectives* coll) {
       return SetError(GZ_ERR_INTERNAL, "collectives: wrong variable-size data");
   return GZ_OK;
 }
+
+gz_status gz_rccl_unique_id(uint8_t id[128]) {
+  GZ_CPU_CHECK("rccl_unique_id");
+  if (!id) return SetError(GZ_ERR_INVALID_ARG, "rccl_unique_id: null id");
+  std::string err;
+  if (!gz::RcclUniqueId(id, &err)) return SetError(GZ_ERR_DEVICE, "rccl_unique_id: " + err);
+  return GZ_OK;
+}
+
+gz_status gz_rccl_create(int device, int rank, int world, const uint8_t id[128], gz_rccl** out,
+                         gz_collectives* coll) {
+  GZ_CPU_CHECK("rccl_create");
+  if (!id || !out || !coll || world < 1 || rank < 0 || rank >= world || device < 0)
+    return SetError(GZ_ERR_INVALID_ARG, "rccl_create: bad argument");
+  std::string err;
+  gz::RcclComm* c = gz::RcclCreate(device, rank, world, id, &err);
+  if (!c) return SetError(GZ_ERR_DEVICE, "rccl_create: " + err);
+  *out = reinterpret_cast<gz_rccl*>(c);
+  coll->ctx = c;
+  coll->rank = rank;
+  coll->world = world;
+  coll->allgather = &gz::RcclAllGather;
+  return GZ_OK;
+}
+
+void gz_rccl_destroy(gz_rccl* comm) { gz::RcclDestroy(reinterpret_cast<gz::RcclComm*>(comm)); }
 
 }  // extern "C"

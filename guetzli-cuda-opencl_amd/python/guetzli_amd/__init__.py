@@ -79,7 +79,7 @@ EXPORTED_SYMBOLS = (
     "gz_last_process_detail", "gz_process_rgb_strips", "gz_strip_layout",
     "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode", "gz_comparator_distmap",
     "gz_comparator_compare_blocks", "gz_png_decode", "gz_comparator_compare_rgb",
-    "gz_comparator_compare_blocks_rgb",
+    "gz_comparator_compare_blocks_rgb", "gz_rccl_unique_id", "gz_rccl_create", "gz_rccl_destroy",
 )
 
 _lib = None
@@ -171,6 +171,11 @@ def lib():
                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_Stats)]
     L.gz_strip_layout.argtypes = [i32, i32, i32, i32] + [ctypes.POINTER(i32)] * 4
     L.gz_collectives_selftest.argtypes = [ctypes.POINTER(_Collectives)]
+    L.gz_rccl_unique_id.argtypes = [ctypes.c_char_p]
+    L.gz_rccl_create.argtypes = [i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp),
+                                 ctypes.POINTER(_Collectives)]
+    L.gz_rccl_destroy.argtypes = [vp]
+    L.gz_rccl_destroy.restype = None
     L.gz_profile_enable.argtypes = [i32]
     L.gz_profile_get.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long),
                                  ctypes.POINTER(ctypes.c_double)]
@@ -468,8 +473,41 @@ class Collectives:
 
         return cls(rank, world, allgather_into=allgather_into)
 
+    @classmethod
+    def from_rccl(cls, device, rank, world, unique_id):
+        """The library's own RCCL communicator (gz_rccl_create: staged
+        all-gathers on its own HIP stream, no torch); unique_id: the 128
+        bytes of rccl_unique_id() on one rank, handed to every rank.  close()
+        (or the object's end) destroys the communicator."""
+        obj = cls.__new__(cls)
+        obj.rank, obj.world = rank, world
+        obj._c = _Collectives()
+        h = ctypes.c_void_p()
+        uid = bytes(unique_id)
+        if len(uid) != 128:
+            raise GuetzliError(1, "from_rccl: the unique id has 128 bytes")
+        _check(lib().gz_rccl_create(device, rank, world, uid, ctypes.byref(h), ctypes.byref(obj._c)),
+               "rccl_create")
+        obj._rccl = h.value
+        return obj
+
+    def close(self):
+        if getattr(self, "_rccl", None):
+            lib().gz_rccl_destroy(self._rccl)
+            self._rccl = None
+
+    def __del__(self):
+        self.close()
+
     def selftest(self):
         _check(lib().gz_collectives_selftest(ctypes.byref(self._c)), "collectives_selftest")
+
+
+def rccl_unique_id():
+    """ncclGetUniqueId (gz_rccl_unique_id): 128 bytes for Collectives.from_rccl."""
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().gz_rccl_unique_id(buf), "rccl_unique_id")
+    return buf.raw
 
 
 def strip_layout(width, height, world, rank):

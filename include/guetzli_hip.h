@@ -171,6 +171,20 @@ gz_status gz_strip_layout(int width, int height, int world, int rank, int* y0, i
                           int* e1);
 /* Exercises `coll` (fixed- and variable-size gathers); GZ_OK if consistent. */
 gz_status gz_collectives_selftest(const gz_collectives* coll);
+/* gz_collectives over RCCL (NCCL's API on ROCm: all-gathers over xGMI
+ * between the GPUs of a node), for C/C++ callers running one process per
+ * GPU without torch.distributed (the reference has no collectives,
+ * SURVEY.md §5).  One rank calls gz_rccl_unique_id and
+ * hands the 128 bytes to the others by its own means (MPI, a file, a
+ * socket); every rank then calls gz_rccl_create (ncclCommInitRank: returns
+ * when all have), which fills *coll for gz_process_rgb_strips.  RCCL is
+ * loaded on first use (librccl.so.1).  gz_rccl_destroy after the last
+ * encode that uses *coll. */
+typedef struct gz_rccl gz_rccl;
+gz_status gz_rccl_unique_id(uint8_t id[128]);
+gz_status gz_rccl_create(int device, int rank, int world, const uint8_t id[128], gz_rccl** out,
+                         gz_collectives* coll);
+void gz_rccl_destroy(gz_rccl* comm);
 
 /* ---- comparator (guetzli::ButteraugliComparator) ---------------------- */
 /* ButteraugliComparator(w, h, rgb, target, stats) ctor

@@ -8,7 +8,7 @@
 //
 //   guetzli_ref encode  RGB W H QUALITY OUT.jpg [c|cpu] [lookahead=N new_model=0|1
 //                       try_420=0|1 force_420=0|1]       guetzli.cc:247-368
-//   guetzli_ref stages  RGB W H QSEED OUTDIR                 see Stages()
+//   guetzli_ref stages  RGB W H QSEED OUTDIR [nozero]        see Stages()
 //   guetzli_ref zero_variants RGB W H QSEED OUTDIR           see ZeroVariants()
 //   guetzli_ref encode_jpeg IN.jpg QUALITY OUT.jpg            processor.cc:1029-1066
 //   guetzli_ref decode  IN.jpg OUT.rgb OUT.coeffs             ReadJpeg + DecodeJpegToRGB
@@ -365,8 +365,9 @@ int Stages(int argc, char** argv) {
   }
 
   // Per-block greedy zeroing order, CPU_OPT loop of SelectFrequencyMasking
-  // (processor.cc:641-672) with comp_mask 7, factor 1.
-  {
+  // (processor.cc:641-672) with comp_mask 7, factor 1 (argv[7] "nozero":
+  // skipped -- the frame-size stage hashes, tests/golden/make_stage_hashes.py).
+  if (!(argc > 7 && !strcmp(argv[7], "nozero"))) {
     std::vector<guetzli::CoeffData> out = ZeroOrders(rgb, w, h, target, jpg, &img, 3, 7, true);
     WriteAll(dir + "/zero_order.bin", out.data(), out.size() * sizeof(out[0]));
   }

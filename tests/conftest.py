@@ -101,6 +101,13 @@ def lazy_sort_check_bin():
 
 
 @pytest.fixture(scope="session")
+def collectives_check_bin():
+    """tests/native/collectives_check: StagedAllGather (the RCCL collectives'
+    buffer handling) over a host-memory transport."""
+    return _native_bin("collectives_check", False)
+
+
+@pytest.fixture(scope="session")
 def pool_check_bin():
     """tests/native/pool_check: the shared host worker pool under concurrency."""
     return _native_bin("pool_check", False)

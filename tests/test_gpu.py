@@ -518,3 +518,44 @@ def test_backend_variants_keep_known_answer(env):
     assert res.returncode == 0, res.stderr[-2000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["sha"] == e["sha256"] and out["iters"] == e["iters"], out
+
+
+_ZIGZAG = [0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24,
+           31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47, 50, 56,
+           59, 61, 35, 36, 48, 49, 57, 58, 62, 63]
+
+
+def _make_q(seed):
+    """oracle/ref_driver.cc MakeQ: the stage fixtures' quantization matrix."""
+    s = (2463534242 ^ (seed * 7919)) & 0xffffffff
+    q = np.zeros((3, 64), np.int32)
+    for c in range(3):
+        for k in range(64):
+            s ^= (s << 13) & 0xffffffff
+            s ^= s >> 17
+            s ^= (s << 5) & 0xffffffff
+            q[c, k] = 1 + (_ZIGZAG[k] * (2 + c)) // 8 + s % 3
+    return q
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST.get("stage_hashes", {})))
+def test_compare_stages_at_frame_size(gz, name):
+    """Every Butteraugli intermediate of one Compare at the BASELINE frame
+    sizes (configs[1] 1080p, configs[2] 4K) bit-identical to the
+    reference's (tolerance 0; north_star asks for 1e-5): the reference's
+    stage planes are committed as sha256 (tests/golden/make_stage_hashes.py),
+    the device's are hashed the same way.  This pins the 4K-specific
+    segment, strip and blur-group tiling and every distmap pixel, not only
+    each block's maximum."""
+    e = MANIFEST["stage_hashes"][name]
+    w, h = e["w"], e["h"]
+    rgb = gz.synthetic_frame(e["seed"], w, h)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == e["input_sha256"]
+    cand = _quantized(gz, rgb, w, h, _make_q(e["qseed"])).reshape(-1)
+    assert hashlib.sha256(cand.tobytes()).hexdigest() == e["sha256"]["cand_coeffs"]
+    cmp = gz.ButteraugliComparator(w, h, rgb, e["target"])
+    st = cmp.compare_stages(cand)
+    bad = [k for k in STAGES
+           if hashlib.sha256(np.ascontiguousarray(st[k], np.float32).tobytes()).hexdigest() != e["sha256"][k]]
+    assert not bad, "stages differing from the reference at %dx%d: %s" % (w, h, bad)
+    assert np.float32(st["distance"]) == np.float32(e["distance"])

@@ -208,3 +208,12 @@ def test_speculative_tail_batches_bit_exact(host_e2e_bin, decades, tmp_path):
     assert res.returncode == 0, res.stderr
     assert json.loads(res.stdout)["iters"] == e["iters"]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == e["sha256"]
+
+
+def test_staged_allgather_buffer_handling(collectives_check_bin):
+    """host/rccl_collectives.h: the native RCCL gz_collectives' staging
+    (grow-only device / pinned buffers, zero-byte exchanges, rank order,
+    the variable-size gather on top, every buffer freed) over a host-memory
+    transport with three ranks as threads."""
+    res = subprocess.run([collectives_check_bin], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0 and res.stdout.startswith("ok"), res.stdout + res.stderr

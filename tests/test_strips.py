@@ -227,3 +227,69 @@ def test_gpu_strips_reproduce_reference(name, world):
     for p in procs:
         p.join(60)
     assert len(res) == world and all(v == e["sha256"] for v in res.values()), res
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_reproduce_reference(gz):
+    """The library's own RCCL communicator (gz_rccl_create: host/
+    rccl_collectives.cc, staged all-gathers on its own stream) as the strips'
+    exchange: its self-test and a strip encode over it give the reference's
+    bytes.  World 1 (one GPU on the test box: RCCL refuses two ranks on one
+    device); the multi-GPU wiring is the same calls with more ranks."""
+    e = MANIFEST["e2e"]["bees_q95"]
+    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
+    uid = gz.rccl_unique_id()
+    assert len(uid) == 128
+    coll = gz.Collectives.from_rccl(0, 0, 1, uid)
+    try:
+        coll.selftest()
+        data = gz.process_strips(rgb, e["w"], e["h"], coll, gz.Params.for_quality(e["quality"]), device=0)
+    finally:
+        coll.close()
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]
+
+
+def _bench_strip_rank(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import bench
+    import guetzli_amd as gz
+    torch.set_num_threads(1)
+    dist = None
+    try:
+        _, _, _, dist = bench.dist_setup(world, backend="gloo")
+        # every rank on cuda:0: the leg's group of ranks 0-3, its "cuda:0"
+        # Collectives.from_torch branch and its max-over-ranks time
+        q.put((rank, bench.large_frame(gz, dist, world, rank, 0, w=640, h=360, q=95, seed=3)))
+    except Exception as ex:  # reported to the parent
+        q.put((rank, repr(ex)))
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_bench_large_frame_strip_leg_world4():
+    """bench.py's configs[4] leg as the driver's N >= 4 run takes it --
+    dist.new_group([0, 1, 2, 3]), Collectives.from_torch(dist, "cuda:N",
+    group=...), the all_reduce(MAX) of the time -- with 4 gloo ranks sharing
+    cuda:0 and a small known-answer frame (640x360 q95 seed 3, 4 strips of
+    96 rows + halo): every rank reports the reference's bytes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_strip_rank, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert len(res) == 4, res
+    for r, v in res.items():
+        assert isinstance(v, dict), (r, v)
+        assert v["gpus"] == 4 and "strips" in v["mode"] and v["bit_exact"], (r, v)

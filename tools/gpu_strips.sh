@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 configs[4] check on one GPU box: the single engine vs the strip
+# configs[4] check on one GPU box: the single engine vs the strip
 # split (world 1, and 4 ranks sharing device 0 over gloo), warm, 8192^2 q84.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/strips_r4
+O=gpurun_out/strips_${GZ_TAG:-r5}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python tools/strip_bench.py --warmup 1 --check > $O/w1.json 2> $O/w1.err || { tail -20 $O/w1.err; exit 1; }
