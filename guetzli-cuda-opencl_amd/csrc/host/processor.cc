@@ -672,6 +672,18 @@ bool HipButteraugliComparator::DeviceSelectWindow(size_t from, size_t window, in
   return true;
 }
 
+bool HipButteraugliComparator::DeviceBulkApplyLocal(const CoeffImage& img, int direction, const uint8_t* cnt,
+                                                    const std::vector<int>& last_indexes, int32_t delta[3][256]) {
+  const auto t0 = Clock::now();
+  if (!SyncCoeffs(img)) return false;
+  if (!engine_->BulkApply(direction, img.quant, cnt, delta, &last_indexes)) {
+    err_ = engine_->error();
+    return false;
+  }
+  seconds_bulk += Since(t0);
+  return true;
+}
+
 bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt,
                                                JpegHistogram ac[3]) {
   const auto t0 = Clock::now();
@@ -1803,7 +1815,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // the frame's candidates and block maxima are resident) unless the frame
   // is split over ranks or the comparator has no device
   bool device_order = false;
-  if (!part_ && cmp_->HasDeviceBulk() && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
+  if ((!part_ || part_->world == 1) && cmp_->HasDeviceBulk() && !cmp_->DeviceOrderReset(&device_order))
+    return Fail(err);
   // With the device order the bulk prefix is selected and applied on the
   // device too (DeviceSelectBulk), with the change of the AC histograms
   // counted there.
@@ -1814,10 +1827,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // host copy reflects, is brought up to date (materialize) before the tail
   // reads or changes the block.
   const bool device_bulk = device_order && cmp_->HasDeviceBulk();
+  // A frame split over ranks applies its owned blocks' bulk prefix on its
+  // own device too (from the host's counts and last_indexes), its host copy
+  // then following lazily as with the device order -- except the blocks
+  // within the halo band of a strip edge, which the neighbours' halos need:
+  // those are brought up to date and journalled at once (SyncHalo ships the
+  // journal).  (GZ_STRIP_HOST_BULK=1: the host applies it, for A/B runs.)
+  static const bool strip_host_bulk = getenv("GZ_STRIP_HOST_BULK") && atoi(getenv("GZ_STRIP_HOST_BULK")) != 0;
+  const bool strip_bulk = part_ && !strip_host_bulk && cmp_->HasDeviceBulkLocal();
+  const bool lazy_host = device_bulk || strip_bulk;
   std::vector<int> mat_li;
   std::vector<uint8_t> bulk_cnt8;
-  if (device_bulk) mat_li.assign(num_blocks, 0);
-  auto materialize = [&](int bix) {
+  if (lazy_host) mat_li.assign(num_blocks, 0);
+  auto materialize = [&](int bix, bool journal = false) {
     int m = mat_li[bix];
     const int li = last_indexes[bix];
     if (m == li) return;
@@ -1832,6 +1854,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         v = QuantizeCoeff(comp.coeffs[static_cast<size_t>(by * comp.width_in_blocks + bx) * 64 + k], img->quant[c][k]);
       }
       img->block(c, bix)[k] = v;
+      if (journal) img->MarkChanged(c, bix, k);
       uint64_t& nzm = acm.nz[static_cast<size_t>(c) * num_blocks + bix];
       const int z = kJPEGZigZagOrder[k];
       if (v) nzm |= 1ull << z; else nzm &= ~(1ull << z);
@@ -1954,8 +1977,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         if (!cmp_->DeviceSelectBulk(*img, bulk, kTailWindow, direction, &sel, ac_now)) return Fail(err);
         if (bulk && sel.applied) {
           for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
+          // (the counts include the tie block's share of the K*-keyed entries)
           for (int bix = 0; bix < num_blocks; ++bix) last_indexes[bix] += sel.cnt[bix] * direction;
-          if (sel.tie_block >= 0) last_indexes[sel.tie_block] += sel.take * direction;
           img->host_partial = true;
           refresh_raw();
           loop.changed = static_cast<int>(bulk);
@@ -2015,12 +2038,49 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             }
           });
         }
+        if (strip_bulk) {
+          // the owned blocks' prefix on this rank's device; its histogram
+          // delta summed over the ranks
+          const auto td = Clock::now();
+          bulk_cnt8.assign(num_blocks, 0);
+          for (int bix = own_lo; bix < own_hi; ++bix) bulk_cnt8[bix] = static_cast<uint8_t>(bulk_cnt_[bix]);
+          int32_t delta[3][256] = {};
+          // (a failure on one rank fails every rank at the all-sum below:
+          // its status travels with the delta)
+          const bool ok = cmp_->DeviceBulkApplyLocal(*img, direction, bulk_cnt8.data(), last_indexes, delta);
+          std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1) + 1, 0);
+          for (int c = 0; c < ncomp && c < 3; ++c)
+            for (int q = 0; q + 1 < JpegHistogram::kSize; ++q) hsum[c * (JpegHistogram::kSize - 1) + q] = delta[c][q];
+          hsum.back() = ok ? 0 : 1;
+          if (!part_->SumAll(hsum.data(), static_cast<int>(hsum.size()))) return exchange_failed();
+          if (!ok) return Fail(err);
+          if (hsum.back()) {
+            if (err) *err = "a rank's device bulk prefix failed";
+            return false;
+          }
+          for (int bix = own_lo; bix < own_hi; ++bix) last_indexes[bix] += bulk_cnt_[bix] * direction;
+          img->host_partial = true;
+          // the halo bands' blocks now, journalled (the neighbours' halos)
+          const int band = (kStripHalo / 8) * block_width;
+          for (int bix = own_lo; bix < std::min(own_hi, own_lo + band); ++bix) materialize(bix, true);
+          for (int bix = std::max(own_lo + band, own_hi - band); bix < own_hi; ++bix) materialize(bix, true);
+          // (the counts are stored doubled, JpegHistogram::Add)
+          for (int c = 0; c < ncomp && c < 3; ++c)
+            for (int q = 0; q + 1 < JpegHistogram::kSize; ++q)
+              ac_histograms[c].counts[q] += 2u * static_cast<uint32_t>(hsum[c * (JpegHistogram::kSize - 1) + q]);
+          refresh_raw();
+          loop.changed = static_cast<int>(bulk);
+          res_->detail["backend_bulk_s"] += Since(tbk);
+          res_->detail["backend_bulk_device_s"] += Since(td);
+          res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
+          res_->detail["backend_bulk_device"] += 1;
+        }
         struct ChunkDelta {
           JpegHistogram h[3];
           std::vector<uint32_t> changed;
         };
-        std::vector<ChunkDelta> deltas(own_chunks);
-        ParallelFor(own_chunks, [&](int ch) {
+        std::vector<ChunkDelta> deltas(strip_bulk ? 0 : own_chunks);
+        if (!strip_bulk) ParallelFor(own_chunks, [&](int ch) {
           ChunkDelta& d = deltas[ch];
           int64_t raw_unused = 0;
           const int b0 = own_lo + ch * kOrderChunk, b1 = std::min(own_hi, b0 + kOrderChunk);
@@ -2081,7 +2141,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             last_indexes[bix] = li;
           }
         });
-        {
+        if (!strip_bulk) {
         // (symbols only: the last slot is the histogram's fixed sentinel count)
         std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1), 0);
         for (const ChunkDelta& d : deltas) {
@@ -2105,25 +2165,90 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       double codes_s = 0.0;
       int n_codes = 0;
       double sort_s = 0.0;
-      // one change's bookkeeping after it was applied: the decade's codes,
-      // the estimate and the break test; true: stop after change i
-      auto after_change = [&](size_t i, float key) -> bool {
-        loop.Applied(key);
-        if (loop.CodesRead(i)) {
-          const auto te = Clock::now();
-          ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
-          refresh_raw();
-          codes_s += Since(te);
-          ++n_codes;
+      // The bookkeeping of steps [i0, i0 + n) whose changes' symbol updates
+      // are known (step k: component comp[k], updates logs[k]; key keys[k]),
+      // in speculative batches.  The entropy codes read at step i (i % 10
+      // == 0) are a function of the AC histograms after step i alone, and
+      // the histograms after every step follow from the steps' symbol
+      // updates, which need no codes.  So the histograms are advanced over
+      // the steps first, copied at every step whose codes are read, those
+      // codes built on the pool at once, then the estimate and the break
+      // test run over the steps in order with the same values as the
+      // one-at-a-time loop; the histograms of the steps past
+      // the break are taken back.  Returns the steps processed (through the
+      // break when *stop).
+      struct Snap {
+        size_t step;
+        JpegHistogram h[3];
+        std::vector<uint8_t> depths;
+        int size = 0;
+        int64_t raw[3] = {0, 0, 0};
+      };
+      std::vector<Snap> snaps;
+      auto run_steps = [&](size_t i0, size_t n, const uint8_t* comp, const SymbolLog* logs, const float* keys,
+                           bool* stop) -> size_t {
+        *stop = false;
+        size_t ns = 0;
+        for (size_t k = 0; k < n; ++k) {
+          const SymbolLog& lg = logs[k];
+          for (int e = 0; e < lg.n; ++e) ac_histograms[comp[k]].Add(lg.sym[e], lg.weight[e]);
+          if (loop.CodesRead(i0 + k)) {
+            if (ns == snaps.size()) snaps.emplace_back();
+            Snap& sn = snaps[ns++];
+            sn.step = i0 + k;
+            for (int c = 0; c < ncomp && c < 3; ++c) sn.h[c] = ac_histograms[c];
+          }
         }
-        if (!loop.EstimateRead(i)) return false;
-        est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
-        return loop.Stop(est_jpg_size, prev_size);
+        // (a task takes two consecutive rebuilds: the code-length caches are per thread)
+        if (ns) {
+          const auto te = Clock::now();
+          const int tasks = static_cast<int>((ns + 1) / 2);
+          auto build = [&](int t) {
+            for (size_t q = 2 * static_cast<size_t>(t); q < std::min(ns, 2 * static_cast<size_t>(t) + 2); ++q) {
+              Snap& sn = snaps[q];
+              std::vector<JpegHistogram> hv(sn.h, sn.h + ncomp);
+              sn.size = static_cast<int>(ComputeEntropyCodes(hv, &sn.depths));
+              for (int c = 0; c < ncomp; ++c) sn.raw[c] = HistogramRawBits(sn.h[c], &sn.depths[c * JpegHistogram::kSize]);
+            }
+          };
+          if (tasks == 1) build(0); else ParallelFor(tasks, build);
+          codes_s += Since(te);
+          n_codes += static_cast<int>(ns);
+        }
+        size_t q = 0, k = 0;
+        for (; k < n; ++k) {
+          const size_t s = i0 + k;
+          loop.Applied(keys[k]);
+          if (q < ns && snaps[q].step == s) {
+            const Snap& sn = snaps[q++];
+            ac_histogram_size = sn.size;
+            ac_depths = sn.depths;
+            for (int c = 0; c < ncomp; ++c) raw_bits[c] = sn.raw[c];
+          } else {
+            const SymbolLog& lg = logs[k];
+            const uint8_t* d = &ac_depths[comp[k] * JpegHistogram::kSize];
+            for (int e = 0; e < lg.n; ++e)
+              raw_bits[comp[k]] += static_cast<int64_t>(lg.weight[e]) * (d[lg.sym[e]] + (lg.sym[e] & 0xf));
+          }
+          if (!loop.EstimateRead(s)) continue;
+          est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
+          if (loop.Stop(est_jpg_size, prev_size)) {
+            *stop = true;
+            break;
+          }
+        }
+        if (*stop) {
+          for (size_t u = k + 1; u < n; ++u)
+            for (int e = 0; e < logs[u].n; ++e) ac_histograms[comp[u]].Add(logs[u].sym[e], -logs[u].weight[e]);
+          res_->detail["backend_spec_wasted_codes"] += static_cast<double>(ns - q);
+          return k + 1;
+        }
+        return n;
       };
       // the change of the next entry of owned block bix applied to img: its
       // symbol updates into the frame's histograms, or (log) recorded
       auto apply = [&](int bix, SymbolLog* log) {
-        if (device_bulk) materialize(bix);
+        if (lazy_host) materialize(bix);
         const int bx = bix % block_width, by = bix / block_width;
         const int last_idx = last_indexes[bix];
         const int offset = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
@@ -2143,7 +2268,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
         img->MarkChanged(c, bix, k);
         last_indexes[bix] += direction;
-        if (device_bulk) mat_li[bix] = last_indexes[bix];
+        if (lazy_host) mat_li[bix] = last_indexes[bix];
       };
       if (!part_ || part_->world == 1) {
         // Prefetch window: when the lazy sort hands out a new sorted chunk, the
@@ -2224,21 +2349,14 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         // the pool workers this encode may use), so a tail that stops early
         // wastes at most a few rebuilds.
         struct Spec {
-          int bix, c, k;
+          int bix, k;
           coeff_t old;
           uint64_t nz;
-          float key;
-          SymbolLog log;
-        };
-        struct Snap {
-          size_t step;
-          JpegHistogram h[3];
-          std::vector<uint8_t> depths;
-          int size = 0;
-          int64_t raw[3] = {0, 0, 0};
         };
         std::vector<Spec> spec;
-        std::vector<Snap> snaps;
+        std::vector<uint8_t> sp_comp;
+        std::vector<SymbolLog> sp_log;
+        std::vector<float> sp_key;
         const int workers = std::max(1, PoolWorkerCap());
         constexpr int kMaxDecades = 32;
         // (GZ_SPEC_DECADES: a fixed batch, for A/B runs and tests)
@@ -2250,7 +2368,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           const size_t first_code = (i + 9) / 10 * 10;
           const size_t j = std::min(n_order, first_code + 10 * static_cast<size_t>(decades));
           spec.clear();
-          size_t ns = 0;
+          sp_comp.clear();
+          sp_log.clear();
+          sp_key.clear();
           // A: the batch's changes, their symbol updates into the histograms
           for (size_t s = i; s < j; ++s) {
             if (!tail_ready(s)) return Fail(err);
@@ -2259,7 +2379,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
               prefetch_chunk(s, std::min(prefetched, n_order));
             }
             const int bix = tail_block(s);
-            if (device_bulk) materialize(bix);
+            if (lazy_host) materialize(bix);
             const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
             const int li = last_indexes[bix] + std::min(direction, 0);
             if (li < 0 || off + li >= offsets[bix + 1]) {  // (an order entry without a candidate: a bug)
@@ -2269,73 +2389,30 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             const int idx = cand[off + li];
             Spec sp;
             sp.bix = bix;
-            sp.c = idx / kDCTBlockSize;
+            const int c = idx / kDCTBlockSize;
             sp.k = idx % kDCTBlockSize;
-            sp.old = img->block(sp.c, bix)[sp.k];
-            sp.nz = acm.nz[static_cast<size_t>(sp.c) * num_blocks + bix];
-            sp.key = tail_key(s);
-            apply(bix, &sp.log);
-            for (int e = 0; e < sp.log.n; ++e) ac_histograms[sp.c].Add(sp.log.sym[e], sp.log.weight[e]);
+            sp.old = img->block(c, bix)[sp.k];
+            sp.nz = acm.nz[static_cast<size_t>(c) * num_blocks + bix];
+            sp_log.emplace_back();
+            apply(bix, &sp_log.back());
             spec.push_back(sp);
-            if (loop.CodesRead(s)) {
-              if (ns == snaps.size()) snaps.emplace_back();
-              Snap& sn = snaps[ns++];
-              sn.step = s;
-              for (int c = 0; c < ncomp && c < 3; ++c) sn.h[c] = ac_histograms[c];
-            }
+            sp_comp.push_back(static_cast<uint8_t>(c));
+            sp_key.push_back(tail_key(s));
           }
-          // B: the codes of every read step, on the pool (a task takes two
-          // consecutive ones: the code-length caches are per thread)
-          if (ns) {
-            const auto te = Clock::now();
-            const int tasks = static_cast<int>((ns + 1) / 2);
-            ParallelFor(tasks, [&](int t) {
-              for (size_t q = 2 * static_cast<size_t>(t); q < std::min(ns, 2 * static_cast<size_t>(t) + 2); ++q) {
-                Snap& sn = snaps[q];
-                std::vector<JpegHistogram> hv(sn.h, sn.h + ncomp);
-                sn.size = static_cast<int>(ComputeEntropyCodes(hv, &sn.depths));
-                for (int c = 0; c < ncomp; ++c)
-                  sn.raw[c] = HistogramRawBits(sn.h[c], &sn.depths[c * JpegHistogram::kSize]);
-              }
-            });
-            codes_s += Since(te);
-            n_codes += static_cast<int>(ns);
-          }
-          // C: the estimate and the break test in order
-          size_t q = 0, s = i;
-          for (; s < j; ++s) {
-            const Spec& sp = spec[s - i];
-            loop.Applied(sp.key);
-            if (q < ns && snaps[q].step == s) {
-              const Snap& sn = snaps[q++];
-              ac_histogram_size = sn.size;
-              ac_depths = sn.depths;
-              for (int c = 0; c < ncomp; ++c) raw_bits[c] = sn.raw[c];
-            } else {
-              const uint8_t* d = &ac_depths[sp.c * JpegHistogram::kSize];
-              for (int e = 0; e < sp.log.n; ++e)
-                raw_bits[sp.c] += static_cast<int64_t>(sp.log.weight[e]) * (d[sp.log.sym[e]] + (sp.log.sym[e] & 0xf));
-            }
-            if (!loop.EstimateRead(s)) continue;
-            est_jpg_size = jpg_header_size + dc_size + ac_histogram_size + EntropySizeFromRaw(raw_bits);
-            if (loop.Stop(est_jpg_size, prev_size)) {
-              stop = true;
-              break;
-            }
-          }
+          // B, C: the histograms, the codes of every read step (on the pool),
+          // the estimate and the break test; the changes past the break undone
+          // (newest first; their journal entries stay: they name positions
+          // whose values are current)
+          const size_t done = run_steps(i, j - i, sp_comp.data(), sp_log.data(), sp_key.data(), &stop);
           if (stop) {
-            // undo the changes after the break (newest first)
-            for (size_t u = j; u-- > s + 1;) {
-              const Spec& sp = spec[u - i];
-              img->block(sp.c, sp.bix)[sp.k] = sp.old;
-              acm.nz[static_cast<size_t>(sp.c) * num_blocks + sp.bix] = sp.nz;
+            for (size_t u = j - i; u-- > done;) {
+              const Spec& sp = spec[u];
+              img->block(sp_comp[u], sp.bix)[sp.k] = sp.old;
+              acm.nz[static_cast<size_t>(sp_comp[u]) * num_blocks + sp.bix] = sp.nz;
               last_indexes[sp.bix] -= direction;
-              if (device_bulk) mat_li[sp.bix] = last_indexes[sp.bix];
-              for (int e = 0; e < sp.log.n; ++e) ac_histograms[sp.c].Add(sp.log.sym[e], -sp.log.weight[e]);
-              // (its journal entry stays: it names a position whose value is current)
+              if (lazy_host) mat_li[sp.bix] = last_indexes[sp.bix];
             }
-            res_->detail["backend_spec_undone"] += static_cast<double>(j - s - 1);
-            res_->detail["backend_spec_wasted_codes"] += static_cast<double>(ns - q);
+            res_->detail["backend_spec_undone"] += static_cast<double>(j - i - done);
           }
           i = j;
           if (!fixed_decades) decades = std::min(std::min(kMaxDecades, std::max(4, 2 * workers)), decades * 2);
@@ -2361,6 +2438,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           for (size_t j = 0; j < W; ++j) {
             const int bix = blocks[j] - gbase;
             if (bix < own_lo || bix >= own_hi) continue;
+            if (lazy_host) materialize(bix);  // (the undo records current values)
             const int off = std::max(0, std::min(offsets[bix], static_cast<int>(cand.size()) - 1));
             const int idx = cand[off + last_indexes[bix] + std::min(direction, 0)];
             const int c = idx / kDCTBlockSize, k = idx % kDCTBlockSize;
@@ -2391,26 +2469,36 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
               at[pos] = p + 4;
               p += 6 + 2 * p[5];
             }
-          size_t j = 0;
-          for (; j < W; ++j) {
-            const uint8_t* r = at[j];
-            if (!r) return false;
-            const int c = r[0];
+          // every rank runs the window's bookkeeping from the owners' symbol
+          // updates (the speculative batches of the single-rank tail)
+          std::vector<uint8_t> comp(W);
+          std::vector<SymbolLog> logs(W);
+          for (size_t q = 0; q < W; ++q) {
+            const uint8_t* r = at[q];
+            if (!r || r[1] > 32) return false;
+            comp[q] = r[0];
+            logs[q].n = r[1];
             for (int e = 0; e < r[1]; ++e) {
-              const int sym = r[2 + 2 * e], w = static_cast<int8_t>(r[3 + 2 * e]);
-              ac_histograms[c].Add(sym, w);
-              raw_bits[c] += static_cast<int64_t>(w) * (ac_depths[c * JpegHistogram::kSize + sym] + (sym & 0xf));
+              logs[q].sym[e] = r[2 + 2 * e];
+              logs[q].weight[e] = static_cast<int8_t>(r[3 + 2 * e]);
             }
-            if (after_change(i0 + j, keys[j])) {
-              *stop = true;
-              break;
-            }
+          }
+          size_t j = 0;
+          for (size_t q0 = 0; q0 < W && !*stop;) {
+            // (batches of about kMaxDecades rebuilds, ending before a read step)
+            const size_t i = i0 + q0;
+            const size_t first_code = (i + 9) / 10 * 10;
+            const size_t q1 = std::min(W, first_code + 10 * 32 - i0);
+            const size_t d = run_steps(i, q1 - q0, comp.data() + q0, logs.data() + q0, keys + q0, stop);
+            q0 += d;
+            j = q0 - (*stop ? 1 : 0);
           }
           if (*stop) {
             for (auto u = undo.rbegin(); u != undo.rend() && u->i > i0 + j; ++u) {
               img->block(u->c, u->bix)[u->k] = u->old;
               acm.nz[static_cast<size_t>(u->c) * num_blocks + u->bix] = u->nz;
               last_indexes[u->bix] -= direction;
+              if (lazy_host) mat_li[u->bix] = last_indexes[u->bix];
             }
           }
           *done = *stop ? j + 1 : W;
@@ -2486,7 +2574,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       prev_size = est_jpg_size;
     }
   }
-  if (device_bulk) {
+  if (lazy_host) {
     // the device copy is the image now; nothing after the back end reads
     // the host copy before the next bulk rewrite (CopyFromJpegData) -- a
     // mirror that would have to read it fails instead (host_valid)

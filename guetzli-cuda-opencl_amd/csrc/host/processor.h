@@ -163,6 +163,14 @@ class Comparator {
   virtual bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) {
     return false;
   }
+  // The same without the device order (a frame split over ranks): from the
+  // host's last_indexes; delta[c][symbol] (unscaled) the change of the AC
+  // symbol counts of the changed blocks, for the caller to sum over ranks.
+  virtual bool HasDeviceBulkLocal() const { return false; }
+  virtual bool DeviceBulkApplyLocal(const CoeffImage& img, int direction, const uint8_t* cnt,
+                                    const std::vector<int>& last_indexes, int32_t delta[3][256]) {
+    return false;
+  }
   // Makes the q=1 coefficients of the original image available to
   // QuantizeFromOriginal / BlockZeroingOrders.
   virtual bool SetOriginalCoeffs(const JpegData& jpg) = 0;
@@ -278,6 +286,9 @@ class HipButteraugliComparator : public Comparator {
                                    const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
                                    double best_score, size_t* size, bool* skipped) override;
   bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) override;
+  bool HasDeviceBulkLocal() const override { return true; }
+  bool DeviceBulkApplyLocal(const CoeffImage& img, int direction, const uint8_t* cnt,
+                            const std::vector<int>& last_indexes, int32_t delta[3][256]) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   bool SetOriginalCoeffs420(const JpegData& jpg420) override;
   bool Compare420(const Image420& img) override;

@@ -124,6 +124,44 @@ class PartitionComparator : public Comparator {
                                           const std::vector<float>& max_dist_per_block,
                                           std::vector<float>* block_weight) override;
   bool SetOriginalCoeffs(const JpegData& jpg) override;
+  // One rank (the degenerate split: no halo, the strip is the frame): the
+  // whole device change order and bulk prefix are the inner comparator's.
+  bool HasDeviceBulk() const override { return part_->world == 1 && inner_->HasDeviceBulk(); }
+  bool DeviceOrderReset(bool* available) override {
+    *available = false;
+    if (part_->world != 1) return true;
+    return inner_->DeviceOrderReset(available) || Fail(inner_->error());
+  }
+  bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
+                         float floor_limit, size_t* n_entries, int* blocks_to_change, int64_t* below_floor) override {
+    return inner_->DeviceChangeOrder(direction, target_mul, zero_bmax, last_indexes, floor_limit, n_entries,
+                                     blocks_to_change, below_floor) ||
+           Fail(inner_->error());
+  }
+  bool DeviceOrderEntries(std::vector<std::pair<int, float>>* order) override {
+    return inner_->DeviceOrderEntries(order) || Fail(inner_->error());
+  }
+  bool DeviceSelectBulk(const CoeffImage& img, size_t bulk, size_t window, int direction,
+                        Engine::OrderSelection* sel, JpegHistogram ac[3]) override {
+    return inner_->DeviceSelectBulk(img, bulk, window, direction, sel, ac) || Fail(inner_->error());
+  }
+  bool DeviceSelectWindow(size_t from, size_t window, int direction, Engine::OrderSelection* sel) override {
+    return inner_->DeviceSelectWindow(from, window, direction, sel) || Fail(inner_->error());
+  }
+  bool DeviceBulkApply(const CoeffImage& img, int direction, const uint8_t* cnt, JpegHistogram ac[3]) override {
+    return inner_->DeviceBulkApply(img, direction, cnt, ac) || Fail(inner_->error());
+  }
+  bool DeviceOrderAdvance(float val_threshold, int direction) override {
+    return inner_->DeviceOrderAdvance(val_threshold, direction) || Fail(inner_->error());
+  }
+  // (the owned blocks' bulk prefix on this rank's device: the inner comparator's)
+  bool HasDeviceBulkLocal() const override { return inner_->HasDeviceBulkLocal(); }
+  bool DeviceBulkApplyLocal(const CoeffImage& img, int direction, const uint8_t* cnt,
+                            const std::vector<int>& last_indexes, int32_t delta[3][256]) override {
+    const bool ok = inner_->DeviceBulkApplyLocal(img, direction, cnt, last_indexes, delta);
+    if (!ok) err_ = inner_->error();
+    return ok;
+  }
   const std::string& error() const override { return err_; }
   Comparator* inner() { return inner_.get(); }
   double seconds_exchange = 0.0;

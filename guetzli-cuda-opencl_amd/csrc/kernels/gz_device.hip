@@ -1462,7 +1462,6 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
   if (below_floor) *below_floor = *host_floor;
   ord_n_ = *n_entries;
-  ord_selects_ = 0;
   return true;
 }
 
@@ -1528,7 +1527,8 @@ bool Engine::BulkCountsStaging() {
   return true;
 }
 
-bool Engine::BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel) {
+bool Engine::BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel,
+                              const uint8_t* last8, uint8_t* cnt_host) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const OrdLayout L(nb_);
   QuantMatrix qm;
@@ -1542,19 +1542,33 @@ bool Engine::BulkApplyEnqueue(int direction, const int quant[3][64], const uint8
       std::min(stage_groups, (static_cast<size_t>(nb_) + kBulkWaves - 1) / kBulkWaves));
   GZ_TIMED("bulk_apply", k_bulk_apply<<<groups, kBulkThreads, 0, s>>>(
       cnt_dev, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
-      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_, sel));
+      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_, sel, last8, cnt_host));
   return true;
 }
 
-bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]) {
+bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256],
+                       const std::vector<int>* last_indexes) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
+  if (last_indexes && !d_ord_ && !OrderReset()) return false;  // (the staging for the bytes)
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("BulkApply without a change order", 0);
   if (!BulkCountsStaging()) return false;
   // (the previous BulkApply's kernel, which read the staging, has completed:
   // its histograms were waited for)
   memcpy(h_bulk_, cnt, static_cast<size_t>(nb_));
-  if (!BulkApplyEnqueue(direction, quant, m_bulk_, nullptr)) return false;
+  const uint8_t* last8 = nullptr;
+  if (last_indexes) {
+    if (static_cast<int>(last_indexes->size()) != nb_) return Fail("BulkApply: last indexes", 0);
+    uint8_t* l8 = reinterpret_cast<uint8_t*>(h_ord_);
+    int bad = 0;
+    for (int b = 0; b < nb_; ++b) {
+      bad |= (*last_indexes)[b] & ~0xff;
+      l8[b] = static_cast<uint8_t>((*last_indexes)[b]);
+    }
+    if (bad) return Fail("BulkApply: last index above 255", 0);
+    last8 = reinterpret_cast<const uint8_t*>(m_ord_);
+  }
+  if (!BulkApplyEnqueue(direction, quant, m_bulk_, nullptr, last8, nullptr)) return false;
   // (a sleeping wait: nothing else of this frame is queued behind it)
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
@@ -1571,17 +1585,22 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   const size_t n = ord_n_;
   if (n == 0 || bulk >= n || window == 0) return Fail("OrderSelect arguments", 0);
   if (!BulkCountsStaging()) return false;
-  // (the window is sorted in one workgroup's LDS: at most kSelWindowCap
-  // entries, ties at its keys included; more and the host takes the exact
-  // path)
-  window = std::min<size_t>(window, kSelWindowCap / 2);
-  const size_t cap = kSelWindowCap;
+  // (the candidates -- the window and the ties at its ends -- are sorted in
+  // one workgroup's LDS: at most kSelCandMax; more and the host takes the
+  // exact path)
+  window = std::min<size_t>(window, kSelCandMax / 2);
   if (!h_win_) {
-    GZ_HIP(hipHostMalloc(&h_win_, cap * sizeof(OrderEntry), hipHostMallocCoherent));
+    GZ_HIP(hipHostMalloc(&h_win_, kSelCandMax * sizeof(OrderEntry), hipHostMallocCoherent));
     GZ_HIP(hipHostGetDevicePointer(&m_win_, h_win_, 0));
-    GZ_HIP(hipMalloc(&d_win_, cap * sizeof(OrderEntry)));
-    bytes_ += cap * sizeof(OrderEntry);
+    GZ_HIP(hipMalloc(&d_win_, kSelCandMax * sizeof(unsigned long long)));
+    bytes_ += kSelCandMax * sizeof(unsigned long long);
+    GZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_sel_collect),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(kSelCandMax * sizeof(unsigned long long))));
   }
+  // the sort's capacity: twice the window, 2048 .. kSelCandMax (LDS sized per launch)
+  int cap = 2048;
+  while (static_cast<size_t>(cap) < 2 * window && cap < kSelCandMax) cap <<= 1;
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
   uint32_t* sel = reinterpret_cast<uint32_t*>(base + L.sel);
@@ -1595,41 +1614,37 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   host->done = 0;
   // (GZ_SELECT_OPEN=1: every prefix reported open -- tests of the exact path)
   static const int force_open = getenv("GZ_SELECT_OPEN") ? atoi(getenv("GZ_SELECT_OPEN")) : 0;
-  const unsigned rgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(512, (n + 4095) / 4096)));
-  const unsigned cgroups = static_cast<unsigned>(std::min<size_t>((nb_ + 255) / 256, 64 * 71));
-  // (a later selection over the same build -- the tail's next window --
-  // counts rounds 2 and 3 afresh: round 1's counts are the build's)
-  if (ord_selects_++ > 0)
-    GZ_HIP(hipMemsetAsync(sel + SelLayout::h2, 0, (SelLayout::state - SelLayout::h2) * 4, s));
+  const size_t chunks = (n + 1023) / 1024;
+  const unsigned rgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(512, chunks)));
+  const unsigned cgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(64 * 64, chunks)));
   GZ_TIMED("order_select",
-           (k_sel_round<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), 2, has_prefix, ta, tb, sel),
-            k_sel_round<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), 3, has_prefix, ta, tb, sel),
-            k_sel_classify<<<cgroups, 256, 0, s>>>(e, reinterpret_cast<const int*>(base + L.off), nb_, has_prefix,
-                                                   static_cast<long long>(bulk), ta, tb, sel, cnt8, m_bulk_,
-                                                   static_cast<OrderEntry*>(d_win_), static_cast<int>(cap),
-                                                   mhost, force_open),
-            k_sel_window_sort<<<1, kSelSortThreads, 0, s>>>(static_cast<const OrderEntry*>(d_win_), sel, has_prefix,
-                                                             static_cast<OrderEntry*>(m_win_), mhost)));
-  if (has_prefix && apply && !BulkApplyEnqueue(direction, quant, cnt8, sel)) return false;
+           (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb, sel,
+                                                  reinterpret_cast<uint32_t*>(cnt8), (nb_ + 3) / 4),
+            k_sel_collect<<<cgroups, kSelThreads, static_cast<size_t>(cap) * sizeof(unsigned long long), s>>>(
+                e, static_cast<int>(n), has_prefix, static_cast<long long>(bulk), ta, tb, sel,
+                reinterpret_cast<uint32_t*>(cnt8), static_cast<unsigned long long*>(d_win_), cap,
+                static_cast<OrderEntry*>(m_win_), mhost, force_open)));
+  if (has_prefix && apply && !BulkApplyEnqueue(direction, quant, cnt8, sel, nullptr, m_bulk_)) return false;
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
   if (!host->done) return Fail("OrderSelect: no result", 0);
   out->kbits[0] = host->kbits[0];
   out->kbits[1] = host->kbits[1];
-  out->below = host->below[0];
-  out->eq = host->eq[0];
+  out->below = host->below;
+  out->eq = host->eq;
   out->straddle = host->straddle != 0;
   out->take = host->take;
-  out->tie_block = host->straddle ? host->tie_min : -1;
+  out->tie_block = host->tie_block;
   out->open = host->open != 0;
   out->applied = has_prefix && apply && !out->open;
-  out->window_n = static_cast<size_t>(host->win_n);
-  out->window_overflow = out->window_n > cap;
-  out->window_last = static_cast<size_t>(tb) + 1 >= n;
-  out->cnt.assign(h_bulk_, h_bulk_ + nb_);
+  out->window_n = static_cast<size_t>(host->cand_n);
+  out->window_overflow = host->overflow != 0;
+  out->window_last = host->window_last != 0;
+  if (out->applied) out->cnt.assign(h_bulk_, h_bulk_ + nb_);
+  else out->cnt.clear();
   out->window.clear();
   out->window_ok = 0;
-  if (!out->window_overflow) {
+  if (!out->window_overflow && !out->open) {
     const auto* src = static_cast<const std::pair<int, float>*>(h_win_);
     out->window.assign(src, src + host->win_out);
     out->window_ok = static_cast<size_t>(host->win_ok);

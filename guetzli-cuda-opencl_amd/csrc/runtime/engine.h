@@ -220,7 +220,10 @@ class Engine {
   // OrderBuild, zeroed (direction 1) or restored to Quantize(orig, quant),
   // and the change of every component's AC symbol counts it makes
   // (delta[c][symbol], unscaled), waited for.
-  bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256]);
+  // (last_indexes: the host's, for a back end without the device order --
+  // a frame split over ranks; else the last OrderBuild's copy)
+  bool BulkApply(int direction, const int quant[3][64], const uint8_t* cnt, int32_t delta[3][256],
+                 const std::vector<int>* last_indexes = nullptr);
   // The first `bulk` entries of the last OrderBuild's std::sort order as a
   // set, selected on the device by their keys (radix selection of the key
   // of rank bulk - 1, K*), applied there (k_bulk_apply) -- unless K* is
@@ -236,7 +239,7 @@ class Engine {
     int take = 0;
     int tie_block = -1;          // ... all of tie_block's (when not open)
     bool open = false;
-    bool applied = false;        // the prefix was applied (cnt: per block, tie_block's take not included)
+    bool applied = false;        // the prefix was applied (cnt: per block, tie_block's take included)
     std::vector<uint8_t> cnt;
     size_t window_n = 0;
     bool window_overflow = false;  // more than the staging holds: window empty
@@ -262,7 +265,8 @@ class Engine {
   bool AwaitPosted(const char* h, double* err);
   bool OrderFillEnqueue(size_t grid_entries, float floor_limit);
   bool BulkCountsStaging();
-  bool BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel);
+  bool BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel,
+                        const uint8_t* last8, uint8_t* cnt_host);
   bool Fail(const char* what, int code);
   void ProfBegin(const char* name);
   void ProfEnd();
@@ -371,7 +375,6 @@ class Engine {
   int* h_ord_ = nullptr;            // mapped pinned: last_indexes [nb] | totals [8]
   int* m_ord_ = nullptr;            //   (its device address)
   size_t ord_n_ = 0;                // entries of the last OrderBuild
-  int ord_selects_ = 0;             // OrderSelect calls since it
   void* d_ord_entries_ = nullptr;   // the entries (HBM)
   size_t d_ord_entries_cap_ = 0;
   void* h_ord_entries_ = nullptr;   // pinned: OrderFetch's staging

@@ -16,6 +16,7 @@ import json
 import os
 import socket
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -229,24 +230,43 @@ def test_gpu_strips_reproduce_reference(name, world):
     assert len(res) == world and all(v == e["sha256"] for v in res.values()), res
 
 
+_RCCL_CHILD = r"""
+import hashlib, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import guetzli_amd as gz
+w, h, quality, path, want = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], sys.argv[6]
+rgb = np.fromfile(path, np.uint8)
+uid = gz.rccl_unique_id()
+assert len(uid) == 128
+coll = gz.Collectives.from_rccl(0, 0, 1, uid)
+try:
+    coll.selftest()
+    data = gz.process_strips(rgb, w, h, coll, gz.Params.for_quality(quality), device=0)
+finally:
+    coll.close()
+assert "torch" not in sys.modules
+got = hashlib.sha256(data).hexdigest()
+print(got)
+sys.exit(0 if got == want else 3)
+"""
+
+
 @pytest.mark.gpu
-def test_rccl_collectives_reproduce_reference(gz):
+def test_rccl_collectives_reproduce_reference():
     """The library's own RCCL communicator (gz_rccl_create: host/
     rccl_collectives.cc, staged all-gathers on its own stream) as the strips'
     exchange: its self-test and a strip encode over it give the reference's
     bytes.  World 1 (one GPU on the test box: RCCL refuses two ranks on one
-    device); the multi-GPU wiring is the same calls with more ranks."""
+    device); the multi-GPU wiring is the same calls with more ranks.  In a
+    process of its own without torch, as the C++ callers it serves run: the
+    system RCCL does not initialise beside the ROCm runtime torch bundles
+    (hipGetDeviceCount fails in ncclCommInitRank once torch's is loaded)."""
     e = MANIFEST["e2e"]["bees_q95"]
-    rgb = np.fromfile(os.path.join(GOLDEN, e["input"]), np.uint8)
-    uid = gz.rccl_unique_id()
-    assert len(uid) == 128
-    coll = gz.Collectives.from_rccl(0, 0, 1, uid)
-    try:
-        coll.selftest()
-        data = gz.process_strips(rgb, e["w"], e["h"], coll, gz.Params.for_quality(e["quality"]), device=0)
-    finally:
-        coll.close()
-    assert hashlib.sha256(data).hexdigest() == e["sha256"]
+    r = subprocess.run([sys.executable, "-c", _RCCL_CHILD, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"),
+                        str(e["w"]), str(e["h"]), str(e["quality"]), os.path.join(GOLDEN, e["input"]),
+                        e["sha256"]], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
 def _bench_strip_rank(rank, world, port, q):
