@@ -1328,27 +1328,27 @@ bool Engine::CompactCandidates(int nblocks, float limit, std::vector<int>* offse
 // host takes the exact path (OrderFetch).
 namespace {
 struct OrdLayout {
-  size_t weight, active, cnt, off, info, arr, mbe, last, first, part, sel, cnt8, bytes;
+  size_t weight, active, info, arr, mbe, last, sel, cnt8, bytes;
   explicit OrdLayout(int nb) {
     const size_t n = static_cast<size_t>(nb), a = (n * 4 + 255) / 256 * 256;
     weight = 0;
     active = a;
-    cnt = 2 * a;
-    off = 3 * a;
-    info = off + ((n + 1) * 4 + 255) / 256 * 256;  // 8 ints: per radius blocks with entries, entries
-    arr = info + 256;                               // arrival counters: 1 + groups / 64 + 1
-    mbe = arr + ((n / 256 / 64 + 2) * 4 + 255) / 256 * 256;
+    info = 2 * a;      // (unused; kept zero)
+    arr = info + 256;  // k_order_build's arrival counters: 1 + groups / 64 + 1 (kBuildBlocks per group)
+    mbe = arr + ((n / kBuildBlocks / 64 + 3) * 4 + 255) / 256 * 256;
     last = mbe + a;
-    first = last + a;  // the fill's tile starts: (entries <= 193 n) / 256 + 1 <= n + 4
-    part = first + ((n + 4) * 4 + 255) / 256 * 256;  // 2 ints per counting workgroup
-    sel = part + ((n / 256 + 2) * 8 + 255) / 256 * 256;  // the selection's counts and state
+    sel = last + a;                                         // the selection's counts and state
     cnt8 = sel + (SelLayout::words * 4 + 255) / 256 * 256;  // per-block prefix counts (bytes)
     bytes = cnt8 + (n + 255) / 256 * 256;
   }
 };
 // mapped pinned h_ord_: last_indexes [nb] bytes | totals [8] | below_floor | SelHost
 constexpr int kOrdInfoInts = 8;
-size_t OrdHostBytes(int nb) { return static_cast<size_t>(nb) * 4 + 64 + sizeof(SelHost) + 64; }
+// | per k_order_build workgroup 3 ints
+size_t OrdHostBytes(int nb) {
+  return static_cast<size_t>(nb) * 4 + 64 + (sizeof(SelHost) + 63) / 64 * 64 + 64 +
+         12 * (static_cast<size_t>(nb) / kBuildBlocks + 1);
+}
 }  // namespace
 
 bool Engine::OrderReset(bool* unavailable) {
@@ -1383,6 +1383,9 @@ bool Engine::OrderReset(bool* unavailable) {
     bytes_ += L.bytes;
   }
   GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.mbe, 0, static_cast<size_t>(nb_) * 4, s));
+  // (the selection's counts and state: left zero by every completed build
+  // and selection; cleared per frame so that an abandoned one leaves nothing)
+  GZ_HIP(hipMemsetAsync(static_cast<char*>(d_ord_) + L.sel, 0, L.cnt8 - L.sel, s));
   ord_adv_dir_ = 0;
   ord_n_ = 0;
   return true;
@@ -1407,21 +1410,15 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   hipStream_t s = static_cast<hipStream_t>(stream_);
   GZ_HIP(hipSetDevice(device_));
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderBuild without candidates", 0);
-  // (the fill writes at most cand_n + nb entries: the buffer holds that many
-  // before anything is queued)
+  // (at most cand_n + nb entries: the buffer holds that many before
+  // anything is queued)
   const size_t max_entries = static_cast<size_t>(ord_cand_n_) + static_cast<size_t>(nb_);
   if (!OrderEntriesCapacity(max_entries)) return false;
   if (static_cast<int>(last_indexes.size()) != nb_ || rblock < 1 || rblock > 4)
     return Fail("OrderBuild arguments", 0);
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
-  float* weight = reinterpret_cast<float*>(base + L.weight);
-  int* active = reinterpret_cast<int*>(base + L.active);
   uint32_t* sel = reinterpret_cast<uint32_t*>(base + L.sel);
-  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_, ord_cand_n_, direction,
-                    reinterpret_cast<int*>(base + L.cnt), reinterpret_cast<int*>(base + L.part),
-                    reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
-  const unsigned groups = static_cast<unsigned>((nb_ + 255) / 256);
   int adv_dir = 0;
   if (rblock == 1) {
     // last_indexes change between iterations only: the first radius copies
@@ -1440,51 +1437,50 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
     adv_dir = ord_adv_dir_;
     ord_adv_dir_ = 0;
   }
-  GZ_TIMED("order_build", k_order_local<<<groups, 256, 0, s>>>(d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock,
-                                                                target_distance, weight, active,
-                                                                reinterpret_cast<float*>(base + L.mbe),
-                                                                ord_adv_vt_, adv_dir, rblock == 1 ? 1 : 0, sel,
-                                                                SelLayout::words, a));
-  if (direction < 0) GZ_TIMED("order_build", k_order_near<<<groups, 256, 0, s>>>(active, bw_, bh_, rblock, weight, a));
-  ord_direction_ = direction;
-  // the offsets and the entries queued behind the counts (the fill reads
-  // the total from the offsets; a grid for the largest possible count, its
-  // workgroups past the total leave at once), one wait
-  if (!OrderFillEnqueue(max_entries, floor_limit)) return false;
-  int* host_floor = h_ord_ + nb_ + kOrdInfoInts;
-  if (below_floor) {
-    GZ_HIP(hipMemcpyAsync(host_floor, sel + SelLayout::state + offsetof(SelState, below_floor) / 4, 4,
-                          hipMemcpyDeviceToHost, s));
-  }
+  ord_h1_ ^= 1;  // this build's copy of the round-1 counts (zeroed by the previous build)
+  BuildArgs g;
+  g.bmax = d_block_max_;
+  g.zero_bmax = zero_bmax ? 1 : 0;
+  g.bw = bw_;
+  g.bh = bh_;
+  g.r = rblock;
+  g.direction = direction;
+  g.td = target_distance;
+  g.weight = reinterpret_cast<float*>(base + L.weight);
+  g.active = reinterpret_cast<const int*>(base + L.active);
+  g.mbe = reinterpret_cast<float*>(base + L.mbe);
+  g.adv_vt = ord_adv_vt_;
+  g.adv_dir = adv_dir;
+  g.copy_last = rblock == 1 ? 1 : 0;
+  g.last = reinterpret_cast<int*>(base + L.last);
+  g.last_host = reinterpret_cast<const uint8_t*>(m_ord_);
+  g.off = d_zero_off_;
+  g.cand_n = ord_cand_n_;
+  g.cand_err = d_cand_err_;
+  g.out = static_cast<OrderEntry*>(d_ord_entries_);
+  g.h1 = sel + SelLayout::h1 + ord_h1_ * kSelBins;
+  g.h1_next = sel + SelLayout::h1 + (ord_h1_ ^ 1) * kSelBins;
+  SelState* st = reinterpret_cast<SelState*>(sel + SelLayout::state);
+  g.reserve = &st->reserve[ord_h1_];
+  g.reserve_next = &st->reserve[ord_h1_ ^ 1];
+  const unsigned groups = static_cast<unsigned>((nb_ + kBuildBlocks - 1) / kBuildBlocks);
+  g.wg_host = m_ord_ + nb_ + kOrdInfoInts + 16 + static_cast<int>((sizeof(SelHost) + 63) / 64 * 16);
+  const int* wg = h_ord_ + nb_ + kOrdInfoInts + 16 + static_cast<int>((sizeof(SelHost) + 63) / 64 * 16);
+  g.floor_limit = floor_limit;
+  if (direction < 0)
+    GZ_TIMED("order_build", k_order_active<<<static_cast<unsigned>((nb_ + 255) / 256), 256, 0, s>>>(
+                                d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock, target_distance,
+                                reinterpret_cast<int*>(base + L.active)));
+  GZ_TIMED("order_build", k_order_build<<<groups, 256, 0, s>>>(g));
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
-  *blocks_to_change = h_ord_[nb_ + rblock - 1];
-  *n_entries = static_cast<size_t>(h_ord_[nb_ + 4 + rblock - 1]);
-  if (below_floor) *below_floor = *host_floor;
+  long long tot[3] = {0, 0, 0};
+  for (unsigned k = 0; k < groups; ++k)
+    for (int x = 0; x < 3; ++x) tot[x] += wg[3 * k + x];
+  *blocks_to_change = static_cast<int>(tot[1]);
+  *n_entries = static_cast<size_t>(tot[0]);
+  if (below_floor) *below_floor = tot[2];
   ord_n_ = *n_entries;
-  return true;
-}
-
-// the scan of this build's counts and the fill of up to `grid_entries`
-// entries into HBM (the fill takes the true total from the scan)
-bool Engine::OrderFillEnqueue(size_t grid_entries, float floor_limit) {
-  hipStream_t s = static_cast<hipStream_t>(stream_);
-  const OrdLayout L(nb_);
-  char* base = static_cast<char*>(d_ord_);
-  int* cnt = reinterpret_cast<int*>(base + L.cnt);
-  int* off = reinterpret_cast<int*>(base + L.off);
-  int* first = reinterpret_cast<int*>(base + L.first);
-  const OrderArgs a{reinterpret_cast<int*>(base + L.last), reinterpret_cast<const uint8_t*>(m_ord_), d_zero_off_,
-                    ord_cand_n_, ord_direction_, cnt, reinterpret_cast<int*>(base + L.part),
-                    reinterpret_cast<uint32_t*>(base + L.arr), m_ord_ + nb_};
-  // (the chunk totals from the counting launch's per-workgroup entry totals)
-  if (!ScanCounts(cnt, nb_, off, "order_scan", first, reinterpret_cast<const int*>(base + L.part) + 1))
-    return false;
-  if (grid_entries == 0) return true;
-  GZ_TIMED("order_fill", k_order_fill<<<static_cast<unsigned>((grid_entries + 255) / 256), 256, 0, s>>>(
-      reinterpret_cast<const float*>(base + L.weight), d_cand_err_, reinterpret_cast<const float*>(base + L.mbe), nb_,
-      off, first, static_cast<OrderEntry*>(d_ord_entries_), reinterpret_cast<uint32_t*>(base + L.sel), floor_limit,
-      a));
   return true;
 }
 
@@ -1506,7 +1502,18 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   GZ_HIP(hipMemcpyAsync(h_ord_entries_, d_ord_entries_, bytes, hipMemcpyDeviceToHost, s));
   GZ_HIP(WaitIdle(s));
   ProfFlush();
-  memcpy(static_cast<void*>(out), h_ord_entries_, bytes);
+  // the build groups entries by workgroup in arrival order (blocks in order
+  // within a group, a block's entries in k order): a stable counting sort by
+  // block restores the block order of the host's loop
+  const auto* src = static_cast<const std::pair<int, float>*>(h_ord_entries_);
+  std::vector<int> start(static_cast<size_t>(nb_) + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const int b = src[i].first;
+    if (b < 0 || b >= nb_) return Fail("OrderFetch: entry block", 0);
+    ++start[b + 1];
+  }
+  for (int b = 0; b < nb_; ++b) start[b + 1] += start[b];
+  for (size_t i = 0; i < n; ++i) out[start[src[i].first]++] = src[i];
   return true;
 }
 
@@ -1577,6 +1584,11 @@ bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt
   return true;
 }
 
+// k_sel_collect's dynamic LDS: the sorted keys, the scatter's copy, the bucket counts
+static size_t SelCollectLds(int cap) {
+  return 2 * static_cast<size_t>(cap) * sizeof(unsigned long long) + (kSelSortBins + 1) * sizeof(uint32_t);
+}
+
 bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int quant[3][64], bool apply,
                          OrderSelection* out, int32_t delta[3][256]) {
   hipStream_t s = static_cast<hipStream_t>(stream_);
@@ -1596,10 +1608,10 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
     bytes_ += kSelCandMax * sizeof(unsigned long long);
     GZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_sel_collect),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               static_cast<int>(kSelCandMax * sizeof(unsigned long long))));
+                               static_cast<int>(SelCollectLds(kSelCandMax))));
   }
-  // the sort's capacity: twice the window, 2048 .. kSelCandMax (LDS sized per launch)
-  int cap = 2048;
+  // the sort's capacity: twice the window, 1024 .. kSelCandMax (LDS sized per launch)
+  int cap = 1024;
   while (static_cast<size_t>(cap) < 2 * window && cap < kSelCandMax) cap <<= 1;
   const OrdLayout L(nb_);
   char* base = static_cast<char*>(d_ord_);
@@ -1618,9 +1630,10 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   const unsigned rgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(512, chunks)));
   const unsigned cgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(64 * 64, chunks)));
   GZ_TIMED("order_select",
-           (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb, sel,
+           (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb,
+                                                  sel + SelLayout::h1 + ord_h1_ * kSelBins, sel,
                                                   reinterpret_cast<uint32_t*>(cnt8), (nb_ + 3) / 4),
-            k_sel_collect<<<cgroups, kSelThreads, static_cast<size_t>(cap) * sizeof(unsigned long long), s>>>(
+            k_sel_collect<<<cgroups, kSelThreads, SelCollectLds(cap), s>>>(
                 e, static_cast<int>(n), has_prefix, static_cast<long long>(bulk), ta, tb, sel,
                 reinterpret_cast<uint32_t*>(cnt8), static_cast<unsigned long long*>(d_win_), cap,
                 static_cast<OrderEntry*>(m_win_), mhost, force_open)));

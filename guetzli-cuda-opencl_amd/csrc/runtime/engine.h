@@ -195,18 +195,18 @@ class Engine {
   // processor.cc:776-834, 4:4:4 whole frame) over the candidates of the last
   // BlockZeroingCandidates (HasOrderCandidates) and the block maxima of the
   // last Compare.  OrderReset zeroes max_block_error; OrderBuild computes the
-  // weights at radius rblock (zero_bmax: every block maximum taken as 0),
-  // the entry counts and offsets from last_indexes (host state, uploaded)
-  // and returns their total and the blocks with entries; OrderFetch fills and
-  // downloads the n entries (block, key) in block order; OrderAdvance adds
+  // weights at radius rblock (zero_bmax: every block maximum taken as 0) and
+  // the entries from last_indexes (host state, uploaded) in one launch
+  // (k_order_build) and returns their total and the blocks with entries;
+  // OrderFetch downloads the n entries (block, key) in block order; OrderAdvance adds
   // weight * val_threshold * direction to max_block_error (applied by the
   // next OrderBuild, ahead of its weights).
   bool HasOrderCandidates() const { return ord_cand_n_ >= 0; }
   // (*unavailable: the order's buffers could not be allocated -- the caller
   // builds the order on the host; false is then not returned for it)
   bool OrderReset(bool* unavailable = nullptr);
-  // OrderBuild: the entries of the radius are filled into HBM in block order
-  // (with the selection's first counts); floor_limit > -inf: *below_floor =
+  // OrderBuild: the entries of the radius are filled into HBM, grouped by
+  // workgroup (with the selection's first counts); floor_limit > -inf: *below_floor =
   // the entries keyed below it (the first up iteration's floor).
   bool OrderBuild(int direction, int rblock, double target_distance, bool zero_bmax,
                   const std::vector<int>& last_indexes, size_t* n_entries, int* blocks_to_change,
@@ -263,7 +263,6 @@ class Engine {
   bool OrderEntriesCapacity(size_t n);
   char* RequestStaging(size_t need, char** mapped);  // CompareBlocks* mapped staging
   bool AwaitPosted(const char* h, double* err);
-  bool OrderFillEnqueue(size_t grid_entries, float floor_limit);
   bool BulkCountsStaging();
   bool BulkApplyEnqueue(int direction, const int quant[3][64], const uint8_t* cnt_dev, const uint32_t* sel,
                         const uint8_t* last8, uint8_t* cnt_host);
@@ -368,8 +367,8 @@ class Engine {
   // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
   // max_block_error f32 | last_indexes i32
   int ord_cand_n_ = -1;             // candidates of the last 4:4:4 zeroing search (-1: none)
-  int ord_direction_ = 0;
   float ord_adv_vt_ = 0.0f;         // pending max_block_error update (OrderAdvance)
+  int ord_h1_ = 0;                  // the last build's copy of the selection's round-1 counts
   int ord_adv_dir_ = 0;
   void* d_ord_ = nullptr;
   int* h_ord_ = nullptr;            // mapped pinned: last_indexes [nb] | totals [8]
