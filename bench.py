@@ -87,10 +87,9 @@ def stage_bytes_per_px():
     # S14/S15 + S8 fused: LUT'd mask samples + dc/ac/edge -> R, and the
     # sigma-14 planes (1/16 density) for the low-frequency term
     s["combine_channels"] = (6 * 4 + 9 * 4 + 4) / 9.0 + 6 * 4 / 16.0
-    s["diffmap_blur_h"] = 4 / 9.0 + 4 / 2.0
-    s["diffmap_blur_v"] = 4 / 2.0 + 4 / 4.0
-    s["diffmap_final"] = 4 / 9.0 + 4 / 4.0 + 4 / 64.0
-    s["distance"] = 4 / 64.0                          # the block maxima, read once
+    # S16 + S17 + the distance fused (k_diffmap): the res map in, the block
+    # maxima out (the blur's intermediate planes stay on chip)
+    s["diffmap"] = 4 / 9.0 + 4 / 64.0
     return s
 
 
@@ -106,7 +105,7 @@ ZEROING_BYTES_PER_KEPT = 1 + 4
 # The launches of one search-loop Compare pass (each kernel once; the other
 # entries above are the stage-dump path's or their fused parts).
 PASS_KERNELS = ("coeffs_to_linear", "opsin_mhic", "edge_mask", "block_diff", "blur_h", "blur_v",
-                "combine_channels", "diffmap_blur_h", "diffmap_blur_v", "diffmap_final", "distance")
+                "combine_channels", "diffmap")
 
 
 # The device entropy coder, per MCU (4:4:4: one 8x8 block per component):
@@ -135,13 +134,13 @@ def region_bytes(name, w, h, kept=None):
 # The "blur+mask pass" of BASELINE.json / SURVEY.md 8(d): blurs S1, S4, S7,
 # S16 and the mask chain S9-S13, 272 algorithmic B/px.  Kernels that carry
 # those stages are timed whole (the opsin kernel also does the S2 transform
-# and S3, edge_mask also the S4 blurs, blur_v the S13 LUTs), so the extra
-# fused work only lowers the figure.  ("combine" carries S13 only in the
+# and S3, edge_mask also the S4 blurs, blur_v the S13 LUTs, diffmap also
+# S17, the block maxima and the distance), so the extra fused work only
+# lowers the figure.  ("combine" carries S13 only in the
 # stage-dump path; the search's passes run S14/S15 alone as combine_channels,
 # which is outside the pass.)
 BLUR_MASK_BYTES_PER_PX = 272.0
-BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "diffmap_blur_h",
-                    "diffmap_blur_v")
+BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "diffmap")
 
 # Kernel symbol (rocprofv3 name prefix) of each profiled stage.
 STAGE_SYMBOL = {
@@ -152,12 +151,10 @@ STAGE_SYMBOL = {
     "mask_front": "gz::k_mask_stream(", "edge_mask": "gz::k_edge_mask_stream(",
     "blur_h": "void gz::k_blur_h4<6,", "blur_v": "void gz::k_blur_vstream<6>(",
     "mask_blur_h": "void gz::k_blur_h4<4,", "mask_blur_v": "void gz::k_blur_vstream<4>(",
-    "combine": "gz::k_combine(", "diffmap_blur_h": "void gz::k_blur_h4<5,",
+    "combine": "gz::k_combine(", "diffmap": "gz::k_diffmap(",
     "combine_channels": "gz::k_combine_channels(",
     "block_zeroing": "gz::k_block_zeroing(", "jpeg_stage": "gz::k_jpeg_stage(",
     "jpeg_code": "gz::k_jpeg_code(",
-    "diffmap_blur_v": "void gz::k_blur_vstream<5>(", "diffmap_final": "gz::k_diffmap_final(",
-    "distance": "gz::k_distance(",
 }
 
 

@@ -431,7 +431,6 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   alloc(reinterpret_cast<void**>(&e->d_dc_), 3 * rn * 4);
   alloc(reinterpret_cast<void**>(&e->d_ac_), 3 * rn * 4);
   alloc(reinterpret_cast<void**>(&e->d_resval_), rn * 4);
-  alloc(reinterpret_cast<void**>(&e->d_dd_), n * 4);
   alloc(reinterpret_cast<void**>(&e->d_block_max_), e->nb_ * 4);
   alloc(reinterpret_cast<void**>(&e->d_mask_scale_), 3 * e->nb_ * 4);
   alloc(&e->d_zero_out_, static_cast<size_t>(e->nb_) * 192 * sizeof(CoeffData));
@@ -472,8 +471,11 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_block_max_), e->h_block_max_, 0) != hipSuccess)
     ok = false;
-  alloc(reinterpret_cast<void**>(&e->d_dmax_), 64);  // k_distance's word + arrival counters
-  if (ok && hipMemsetAsync(e->d_dmax_, 0, 64, s) != hipSuccess) ok = false;
+  // k_diffmap's word, the last distance and its arrival counters
+  const size_t dm_groups = static_cast<size_t>((w + kDmTile - 1) / kDmTile) * ((h + kDmTile - 1) / kDmTile);
+  const size_t dm_bytes = 4 * (DmWgMaxOffset(dm_groups) + dm_groups + 4);
+  alloc(reinterpret_cast<void**>(&e->d_dmax_), dm_bytes);
+  if (ok && hipMemsetAsync(e->d_dmax_, 0, dm_bytes, s) != hipSuccess) ok = false;
 
   if (!ok) return fail("device allocation failed");
   // pinned staging (coefficients, offsets, histograms, block maxima)
@@ -650,7 +652,7 @@ Engine::~Engine() {
   if (device_ >= 0) hipSetDevice(device_);
   void* bufs[] = {d_rgb_, d_orig_, d_cur_, d_ref_xyb_, d_lin_, d_xyb_, d_m0_, d_m1_,
                   d_tmp_, d_bl_, d_ma_, d_mb_, d_edge_, d_dc_, d_ac_, d_resval_,
-                  d_dd_, d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
+                  d_block_max_, d_mask_scale_, d_zero_out_, d_scales_,
                   d_zero_count_, d_zero_order_, d_zero_off_, d_cand_idx_, d_cand_err_,
                   d_jhist_, d_jwords_[0], d_jwords_[1], d_jctl_, d_zero_nnz_,
                   d_zero_bins_, d_scan_sums_, d_planes_, d_cand_rgb_, d_ord_, d_dmax_, d_px8_};
@@ -938,24 +940,16 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
         mk, mkdc, d_dc_, d_ac_, d_edge_, w_, h_, rw_, rh_, d_resval_, fuse_lf ? d_bl_ : nullptr,
         fuse_lf ? d_bl_ + 3 * ldn : nullptr));
   }
-  // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map + maxima
+  // S16/S17: diffmap blur on the (w-5)x(h-5) crop, final map, block maxima
+  // and the distance, one launch
   {
-    const int wc = w_ - 5, hc = h_ - 5;
-    BlurPlanes bd{};
-    bd.out[0] = d_tmp_;
-    bd.sig[0] = kSigDiffmap;
-    const dim3 grid9 = BlurH4Grid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_h", k_blur_h4<kBlurDiffmap><<<grid9, 256, 0, s>>>(
-        RowsDiffmap{d_resval_, rw_}, bd, wc, hc, d_scales_, scale_stride_));
-    bd.in[0] = d_tmp_;
-    bd.out[0] = d_dd_;
-    const dim3 grid10 = BlurVStreamGrid(wc, hc, 1, bd);  // fills bp's packed-grid fields
-    GZ_TIMED("diffmap_blur_v", k_blur_vstream<kBlurDiffmap><<<grid10, 256, 0, s>>>(bd, wc, hc, d_scales_, scale_stride_));
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
-    GZ_TIMED("diffmap_final", k_diffmap_final<<<dim3((bw_ + 3) / 4, bh_), 256, 0, s>>>(d_resval_, rw_, d_dd_, w_, h_, bw_,
-                                                              dm, d_block_max_));
-    GZ_TIMED("distance", k_distance<<<kDistGroups, 256, 0, s>>>(d_block_max_, nb_, d_dmax_, m_block_max_ + nb_));
+    const size_t dm_groups = static_cast<size_t>((w_ + kDmTile - 1) / kDmTile) * ((h_ + kDmTile - 1) / kDmTile);
+    GZ_TIMED("diffmap", k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
+                            d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_,
+                            d_dmax_, reinterpret_cast<float*>(d_dmax_ + DmWgMaxOffset(dm_groups)),
+                            m_block_max_ + nb_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");

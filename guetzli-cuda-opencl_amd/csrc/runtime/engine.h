@@ -318,7 +318,6 @@ class Engine {
   float* d_dc_ = nullptr;    // 3R
   float* d_ac_ = nullptr;    // 3R
   float* d_resval_ = nullptr;
-  float* d_dd_ = nullptr;
   float* d_block_max_ = nullptr;
   uint16_t* d_planes_ = nullptr;   // 4:2:0: Cb / Cr pixel state [2][w*h] (allocated on first use)
   uint8_t* d_cand_rgb_ = nullptr;  // sRGB candidate [3*w*h] (allocated on first use)
@@ -362,7 +361,7 @@ class Engine {
   // pinned host staging
   float* h_block_max_ = nullptr;   // pinned: the block maxima on request; [nb_]: the distance (mapped)
   float* m_block_max_ = nullptr;
-  uint32_t* d_dmax_ = nullptr;      // k_distance's maximum word + arrival counters
+  uint32_t* d_dmax_ = nullptr;      // k_diffmap: the last distance, arrival counters, per-workgroup maxima
   // device change order (allocated on first use): weight f32 | active i32 |
   // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
   // max_block_error f32 | last_indexes i32
