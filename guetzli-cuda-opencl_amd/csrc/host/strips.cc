@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "host/jpeg_encode.h"
@@ -769,6 +770,17 @@ int ProcessStrips(int device, const ProcessParams& params, const uint8_t* rgb, i
   if (params.butteraugli_target > 2.0f) {
     if (err) *err = "butteraugli target above 2.0 (quality below 84) is not supported";
     return GZ_ERR_INVALID_ARG;
+  }
+  // One rank: its strip is the frame and there is nothing to exchange -- the
+  // single-engine search, whose bytes the split reproduces (its device
+  // order, known-histogram coding and skipped scans; the strip machinery at
+  // world 1 took 1.28 s for configs[4] against the engine's 1.14).
+  // GZ_STRIP_FORCE=1 keeps the strip machinery, for its tests.
+  static const bool force = getenv("GZ_STRIP_FORCE") && atoi(getenv("GZ_STRIP_FORCE")) != 0;
+  if (coll->world() == 1 && !force) {
+    const int rc = Process(device, params, rgb, false, w, h, result, err);
+    result->detail["strip_single_engine"] = 1;
+    return rc;
   }
   const StripLayout L = StripLayout::Make(w, h, coll->world());
   for (int r = 0; r < coll->world(); ++r)

@@ -187,8 +187,10 @@ def test_torch_collectives_gloo_world2():
     assert res == {0: "ok", 1: "ok"}
 
 
-def _gpu_strip_rank(rank, world, port, e, q):
+def _gpu_strip_rank(rank, world, port, e, q, force=False):
     import sys
+    if force:  # (world 1 runs the strip machinery, not the single-engine search)
+        os.environ["GZ_STRIP_FORCE"] = "1"
     sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
     import torch.distributed as dist
     import guetzli_amd as gz
@@ -210,18 +212,20 @@ def _gpu_strip_rank(rank, world, port, e, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,world", [("bees_q95", 1), ("bees_q90", 2),
-                                        ("synth_8192x8192_s0_q84", 4)])
-def test_gpu_strips_reproduce_reference(name, world):
+@pytest.mark.parametrize("name,world,force", [("bees_q95", 1, True), ("bees_q95", 1, False), ("bees_q90", 2, False),
+                                              ("synth_8192x8192_s0_q84", 4, False)])
+def test_gpu_strips_reproduce_reference(name, world, force):
     """`world` ranks, each a process with its strip's engine on cuda:0, the
     exchange over gloo: every rank returns the reference bytes -- including
-    BASELINE configs[4] (8192x8192 q84 as 4 strips of 2048 rows + halo)."""
+    BASELINE configs[4] (8192x8192 q84 as 4 strips of 2048 rows + halo).  One
+    rank: the single-engine search by default, the strip machinery with
+    GZ_STRIP_FORCE=1 (force)."""
     import torch.multiprocessing as mp
     e = MANIFEST["e2e"].get(name) or MANIFEST["synthetic"][name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_strip_rank, args=(r, world, port, e, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_strip_rank, args=(r, world, port, e, q, force)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
@@ -258,14 +262,17 @@ def test_rccl_collectives_reproduce_reference():
     rccl_collectives.cc, staged all-gathers on its own stream) as the strips'
     exchange: its self-test and a strip encode over it give the reference's
     bytes.  World 1 (one GPU on the test box: RCCL refuses two ranks on one
-    device); the multi-GPU wiring is the same calls with more ranks.  In a
+    device; GZ_STRIP_FORCE=1: the strip machinery, not the single-engine
+    search a one-rank split runs); the multi-GPU wiring is the same calls with
+    more ranks.  In a
     process of its own without torch, as the C++ callers it serves run: the
     system RCCL does not initialise beside the ROCm runtime torch bundles
     (hipGetDeviceCount fails in ncclCommInitRank once torch's is loaded)."""
     e = MANIFEST["e2e"]["bees_q95"]
     r = subprocess.run([sys.executable, "-c", _RCCL_CHILD, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"),
                         str(e["w"]), str(e["h"]), str(e["quality"]), os.path.join(GOLDEN, e["input"]),
-                        e["sha256"]], capture_output=True, text=True, timeout=300)
+                        e["sha256"]], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, GZ_STRIP_FORCE="1"))
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
