@@ -608,8 +608,9 @@ def main():
     ap.add_argument("--quality", type=int, default=95)
     ap.add_argument("--frames-per-step", type=int, default=8,
                     help="frames per GPU per step, encoded concurrently")
-    ap.add_argument("--in-flight", type=int, default=10,
-                    help="frames encoded at once per GPU (0: the frames of one step)")
+    ap.add_argument("--in-flight", type=int, default=8,
+                    help="frames encoded at once per GPU (0: the frames of one step; 8 measured best "
+                         "in round 5, profiles/round5_inflight_sweep.txt)")
     ap.add_argument("--host-threads", type=int, default=0,
                     help="host pool threads per process, caller included (sets GZ_HOST_THREADS "
                          "unless that is set; 0: the library's default, min(16, usable CPUs); "
