@@ -946,10 +946,11 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
     const size_t dm_groups = static_cast<size_t>((w_ + kDmTile - 1) / kDmTile) * ((h_ + kDmTile - 1) / kDmTile);
-    GZ_TIMED("diffmap", k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
-                            d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_,
-                            d_dmax_, reinterpret_cast<float*>(d_dmax_ + DmWgMaxOffset(dm_groups)),
-                            m_block_max_ + nb_));
+    float* wg_max = reinterpret_cast<float*>(d_dmax_ + DmWgMaxOffset(dm_groups));
+    GZ_TIMED("diffmap", (k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
+                             d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_, wg_max),
+                         k_distance<<<1, 256, 0, s>>>(wg_max, static_cast<int>(dm_groups), d_dmax_,
+                                                      m_block_max_ + nb_)));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");
@@ -1537,13 +1538,14 @@ bool Engine::BulkApplyEnqueue(int direction, const int quant[3][64], const uint8
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(quant[c][c_natural_order[k]]);
-  // (at most as many workgroups as the histogram stage has arrival counters)
+  // (round 4 capped the grid at the histogram stage's arrival counters; kept)
   const size_t stage_groups = (3 * static_cast<size_t>(nb_) + kStageBlocks - 1) / kStageBlocks;
   const unsigned groups = static_cast<unsigned>(
       std::min(stage_groups, (static_cast<size_t>(nb_) + kBulkWaves - 1) / kBulkWaves));
   GZ_TIMED("bulk_apply", k_bulk_apply<<<groups, kBulkThreads, 0, s>>>(
       cnt_dev, reinterpret_cast<const int*>(static_cast<char*>(d_ord_) + L.last), d_zero_off_, ord_cand_n_,
-      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, m_jhist_, sel, last8, cnt_host));
+      d_cand_idx_, nb_, direction, d_orig_, qm, qf, d_cur_, d_jhist_, sel, last8, cnt_host),
+      k_hist_fold<<<1, 1024, 0, s>>>(d_jhist_, m_jhist_, 0));
   return true;
 }
 
@@ -1578,7 +1580,7 @@ bool Engine::BulkApply(int direction, const int quant[3][64], const uint8_t* cnt
   return true;
 }
 
-// k_sel_collect's dynamic LDS: the sorted keys, the scatter's copy, the bucket counts
+// k_sel_finish's dynamic LDS: the sorted keys, the scatter's copy, the bucket counts
 static size_t SelCollectLds(int cap) {
   return 2 * static_cast<size_t>(cap) * sizeof(unsigned long long) + (kSelSortBins + 1) * sizeof(uint32_t);
 }
@@ -1600,7 +1602,7 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
     GZ_HIP(hipHostGetDevicePointer(&m_win_, h_win_, 0));
     GZ_HIP(hipMalloc(&d_win_, kSelCandMax * sizeof(unsigned long long)));
     bytes_ += kSelCandMax * sizeof(unsigned long long);
-    GZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_sel_collect),
+    GZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_sel_finish),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                static_cast<int>(SelCollectLds(kSelCandMax))));
   }
@@ -1627,10 +1629,14 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
            (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb,
                                                   sel + SelLayout::h1 + ord_h1_ * kSelBins, sel,
                                                   reinterpret_cast<uint32_t*>(cnt8), (nb_ + 3) / 4),
-            k_sel_collect<<<cgroups, kSelThreads, SelCollectLds(cap), s>>>(
-                e, static_cast<int>(n), has_prefix, static_cast<long long>(bulk), ta, tb, sel,
-                reinterpret_cast<uint32_t*>(cnt8), static_cast<unsigned long long*>(d_win_), cap,
-                static_cast<OrderEntry*>(m_win_), mhost, force_open)));
+            k_sel_collect<<<cgroups, kSelThreads, 0, s>>>(e, static_cast<int>(n), has_prefix,
+                                                           static_cast<long long>(bulk), ta, tb, sel,
+                                                           reinterpret_cast<uint32_t*>(cnt8),
+                                                           static_cast<unsigned long long*>(d_win_), cap),
+            k_sel_finish<<<1, kSelThreads, SelCollectLds(cap), s>>>(
+                static_cast<int>(n), has_prefix, static_cast<long long>(bulk), sel, reinterpret_cast<uint32_t*>(cnt8),
+                static_cast<const unsigned long long*>(d_win_), cap, static_cast<OrderEntry*>(m_win_), mhost,
+                force_open)));
   if (has_prefix && apply && !BulkApplyEnqueue(direction, quant, cnt8, sel, nullptr, m_bulk_)) return false;
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
@@ -1755,10 +1761,11 @@ bool Engine::JpegStageEnqueueRange(const int q[3][64], int m0, int m1) {
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
-  // (the device counts are zero: cleared at creation, and by the last
-  // workgroup of every stage after it has published them to h_jhist_)
-  GZ_TIMED("jpeg_stage", k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, kStageThreads, 0, s>>>(
-      d_cur_, qf, nb_, m0, m1, d_jhist_, m_jhist_));
+  // (the device counts are zero: cleared at creation, and by every fold
+  // after it has published them to h_jhist_)
+  GZ_TIMED("jpeg_stage", (k_jpeg_stage<<<(3 * (m1 - m0) + kStageBlocks - 1) / kStageBlocks, kStageThreads, 0, s>>>(
+                              d_cur_, qf, nb_, m0, m1, d_jhist_),
+                          k_hist_fold<<<1, 1024, 0, s>>>(d_jhist_, m_jhist_, 1)));
   GZ_HIP(hipEventRecord(static_cast<hipEvent_t>(stage_event_), s));
   return true;
 }
@@ -1820,11 +1827,13 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
-  GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
-                                                            static_cast<unsigned long long>(base),
-                                                            pad_end ? 1 : 0, words, ffc, arr, status, side,
-                                                            seam, jepoch_, m_jhist_ + 6 * 256 + 2,
-                                                            d_dmax_ + kDistWord, skip_at));
+  GZ_TIMED("jpeg_code", (k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
+                                                             static_cast<unsigned long long>(base),
+                                                             pad_end ? 1 : 0, words, ffc, status, side, seam,
+                                                             jepoch_, d_dmax_ + kDistWord, skip_at),
+                         k_code_fold<<<1, 64, 0, s>>>(ffc, status, side, groups,
+                                                      static_cast<unsigned long long>(base), pad_end ? 1 : 0,
+                                                      m_jhist_ + 6 * 256 + 2, d_dmax_ + kDistWord, skip_at)));
   jpart_[jslot_].base = base;
   // (0xff count, bit total, shared words) reach h_jhist_[1538..1543] from
   // the last workgroup to finish
