@@ -457,7 +457,9 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
   const size_t jctl_bytes = kCodeFfCopies * 8 + (1 + code_groups / 64 + 2) * 8 + code_groups * 8 +
                             code_groups * 16 + (code_groups + 1) * 4;
   alloc(reinterpret_cast<void**>(&e->d_jctl_), jctl_bytes);
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), 6 * 256 * 4 + 64, hipHostMallocCoherent) != hipSuccess)
+  // (stage counts, chroma count, then the coder's words: kJCodeHost ..)
+  const size_t jhost_bytes = 4 * (kJCodeHost + kCodeHostFf + (static_cast<size_t>(e->nb_) + kCodeMcus - 1) / kCodeMcus + 16);
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_jhist_), jhost_bytes, hipHostMallocCoherent) != hipSuccess)
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_jhist_), e->h_jhist_, 0) != hipSuccess)
     ok = false;
@@ -1819,7 +1821,6 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   // launch counter: tags the status words (low 14 bits)
   if ((++jepoch_ & 0x3fff) == 0) ++jepoch_;  // (0: the zeroed words' tag)
   const size_t max_groups = (static_cast<size_t>(nb_) + kCodeMcus - 1) / kCodeMcus;
-  unsigned long long* ffc = reinterpret_cast<unsigned long long*>(d_jctl_);
   uint32_t* arr = d_jctl_ + 2 * kCodeFfCopies;
   uint64_t* status = reinterpret_cast<uint64_t*>(arr) + 1 + max_groups / 64 + 2;
   uint64_t* side = status + max_groups;
@@ -1827,29 +1828,33 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   JpegQuantF qf;
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 64; ++k) qf.qz[c][k] = static_cast<float>(q[c][c_natural_order[k]]);
-  GZ_TIMED("jpeg_code", (k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
-                                                             static_cast<unsigned long long>(base),
-                                                             pad_end ? 1 : 0, words, ffc, status, side, seam,
-                                                             jepoch_, d_dmax_ + kDistWord, skip_at),
-                         k_code_fold<<<1, 64, 0, s>>>(ffc, status, side, groups,
-                                                      static_cast<unsigned long long>(base), pad_end ? 1 : 0,
-                                                      m_jhist_ + 6 * 256 + 2, d_dmax_ + kDistWord, skip_at)));
+  GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
+                                                            static_cast<unsigned long long>(base),
+                                                            pad_end ? 1 : 0, words, m_jhist_ + kJCodeHost, status,
+                                                            side, seam, jepoch_, d_dmax_ + kDistWord, skip_at));
   jpart_[jslot_].base = base;
-  // (0xff count, bit total, shared words) reach h_jhist_[1538..1543] from
-  // the last workgroup to finish
+  jcode_groups_[jslot_] = groups;
+  jcode_pad_[jslot_] = pad_end;
+  // (the bit total, the shared words and every workgroup's 0xff count reach
+  // h_jhist_ + kJCodeHost from the coder itself)
   return true;
 }
 
 bool Engine::JpegScanFinishPart(ScanPart* part) {
   ScanPart& p = jpart_[jslot_];
-  const uint32_t* h = h_jhist_ + 6 * 256 + 2;
-  p.ff = h[0];
-  p.bits = static_cast<uint64_t>(h[1]) | (static_cast<uint64_t>(h[2]) << 32);
-  p.first_word = h[3];
-  p.last_word = h[4];
-  p.first_shared = (h[5] & 1) != 0;
-  p.last_open = (h[5] & 2) != 0;
-  if (h[5] & 4) return Fail("JpegScan: a part under one word", 0);
+  const uint32_t* h = h_jhist_ + kJCodeHost;
+  p.bits = static_cast<uint64_t>(h[kCodeHostBits]) | (static_cast<uint64_t>(h[kCodeHostBits + 1]) << 32);
+  uint64_t ff = 0;
+  for (int t = 0; t < jcode_groups_[jslot_]; ++t) ff += h[kCodeHostFf + t];
+  p.ff = ff;
+  const uint64_t end = p.base + p.bits;
+  p.first_shared = (p.base & 31) != 0;
+  p.last_open = !jcode_pad_[jslot_] && (end & 31) != 0;
+  p.first_word = p.first_shared ? h[kCodeHostFirst] : 0u;
+  p.last_word = p.last_open ? h[kCodeHostLast] : 0u;
+  // (one word holding both ends of the part -- a part under 32 bits -- is
+  // not supported by the seam exchange)
+  if (p.first_shared && p.bits && (p.base >> 5) == ((end - 1) >> 5)) return Fail("JpegScan: a part under one word", 0);
   if ((p.base % 32 + p.bits + 31) / 32 + 1 > jwords_cap_) return Fail("JpegScan bitstream capacity", 0);
   jnbits_[jslot_] = p.bits;
   if (part) *part = p;

@@ -336,6 +336,8 @@ class Engine {
   uint32_t* d_jwords_[2] = {nullptr, nullptr};  // scan bitstreams: current / kept slot
   uint64_t jnbits_[2] = {0, 0};
   ScanPart jpart_[2];
+  int jcode_groups_[2] = {0, 0};   // the coder launch's workgroups, per slot
+  bool jcode_pad_[2] = {false, false};
   int jslot_ = 0;                  // current slot (kept = jslot_ ^ 1)
   uint32_t* d_jctl_ = nullptr;     //   k_jpeg_code: 0xff counters | arrivals | status | shared words
   uint32_t jepoch_ = 0;            //   launches so far (status tags)
