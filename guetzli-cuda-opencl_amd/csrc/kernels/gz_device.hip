@@ -1183,7 +1183,7 @@ static long long* BzTraceBuf(int nb, void* stream) {
   if (nb > cap) {
     if (buf) hipFree(buf);
     buf = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&buf), static_cast<size_t>(nb) * 32) != hipSuccess) return nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), static_cast<size_t>(nb) * 8 * kBzTraceWords) != hipSuccess) return nullptr;
     cap = nb;
   }
   (void)stream;
@@ -1192,7 +1192,7 @@ static long long* BzTraceBuf(int nb, void* stream) {
 static void BzTraceDump(long long* buf, int nb, void* stream) {
   static const char* path = getenv("GZ_BZ_TRACE");
   if (!buf || !path) return;
-  std::vector<long long> h(static_cast<size_t>(nb) * 4);  // (start, end, steps, list sorted)
+  std::vector<long long> h(static_cast<size_t>(nb) * kBzTraceWords);  // (start, end, steps, list sorted[, phases])
   if (hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)) != hipSuccess ||
       hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess)
     return;

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timeline of one k_block_zeroing launch: encodes a synthetic frame with
 GZ_BZ_TRACE set (the engine records each block's start / end on the 100 MHz
-wall clock, its greedy step count and when its candidate list was sorted) and reports the span, the per-block
+wall clock, its greedy step count and when its candidate list was sorted; with a library built with
+-DGZ_BZ_PHASES also its shader-clock cycles per search phase) and reports the span, the per-block
 duration distribution, how much of the span the longest blocks alone take
 (the launch's critical path) and how many blocks are in flight over time.
 
@@ -27,7 +28,33 @@ def main():
             "rgb = gz.synthetic_frame(0, %d, %d); gz.process(rgb, %d, %d, gz.Params.for_quality(%d))"
             % (os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"), w, h, w, h, q))
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
-    t = np.fromfile(path, dtype=np.int64).reshape(-1, 4)
+    raw = np.fromfile(path, dtype=np.int64)
+    nb = ((w + 7) // 8) * ((h + 7) // 8)
+    words = raw.size // nb
+    t = raw.reshape(nb, words)
+    phases = None
+    if words >= 12:
+        names = ["pixel", "dc_edge_sums", "row_fft", "col_fft", "csf", "ac_lf", "error", "choose_update"]
+        ph = t[:, 4:12].sum(axis=0).astype(np.float64)
+        phases = {n: round(float(v / ph.sum()), 4) for n, v in zip(names, ph)}
+        phases["cycles_per_step"] = round(float(ph.sum() / max(int(t[:, 2].sum()), 1)), 1)
+    census = None
+    if words >= 14:
+        # resident blocks per CU over time from HW_ID (cu 11:8, sh 12, se 15:13)
+        # and XCC_ID: the maximum and the mean at 20 instants
+        hw, xcc = t[:, 12].astype(np.int64), t[:, 13].astype(np.int64) & 0xf
+        cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf)
+        simd = (cu << 2) | ((hw >> 4) & 3)
+        st, en = t[:, 0], t[:, 1]
+        inst = np.linspace(st.min(), en.max(), 22)[1:-1]
+        per_cu, per_simd = [], []
+        for m in inst:
+            live = (st <= m) & (en > m)
+            _, c = np.unique(cu[live], return_counts=True)
+            _, c2 = np.unique(simd[live], return_counts=True)
+            per_cu.append((int(c.max()) if c.size else 0, round(float(c.mean()), 2) if c.size else 0))
+            per_simd.append(int(c2.max()) if c2.size else 0)
+        census = {"cus_seen": int(np.unique(cu).size), "per_cu_max_mean": per_cu, "per_simd_max": per_simd}
     start, end, steps, sorted_t = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
     setup = (sorted_t - start) / 100.0  # us: reference opsin, IDCT, candidate keys + sort
     t0 = start.min()
@@ -56,6 +83,8 @@ def main():
         "last_start_us": round(float(s_us.max()), 1),
         "inflight_over_time": inflight,
         "sum_block_us": round(float(dur.sum()), 0),
+        "phase_share": phases,
+        "census": census,
     }))
 
 
