@@ -1626,7 +1626,13 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   static const int force_open = getenv("GZ_SELECT_OPEN") ? atoi(getenv("GZ_SELECT_OPEN")) : 0;
   const size_t chunks = (n + 1023) / 1024;
   const unsigned rgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(512, chunks)));
-  const unsigned cgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(64 * 64, chunks)));
+  // (k_sel_collect: every workgroup first picks the 24-bit bins from round
+  // 2's counts -- 32 KiB of reads and two barriers -- so the grid stays at
+  // one round of resident 1024-lane workgroups, 2 per CU, each looping over
+  // its share of the entries, instead of one workgroup per 1024 entries: at
+  // 1080p 2050 workgroups paid that pick in 4 rounds)
+  static const size_t cmax = getenv("GZ_SEL_CGROUPS") ? static_cast<size_t>(atoi(getenv("GZ_SEL_CGROUPS"))) : 512;
+  const unsigned cgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(cmax, chunks)));
   GZ_TIMED("order_select",
            (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb,
                                                   sel + SelLayout::h1 + ord_h1_ * kSelBins, sel,
