@@ -166,11 +166,14 @@ __device__ __forceinline__ float masked(float v, bool keep) {
 // Lane shifts by DPP (a VALU modifier, no LDS round trip): wave_next(v) is
 // lane i+1's value in lane i, wave_prev(v) lane i-1's; the edge lane gets 0.
 // Call them with the whole wave active (outside lane-divergent branches).
+// bound_ctrl gives the edge lane its 0 (all rows and banks enabled, the old
+// value is never read): no zeroing move per shift, and the compiler can fold
+// the shift into the instruction that consumes it.
 __device__ __forceinline__ float wave_next(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float wave_prev(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 
 
