@@ -468,14 +468,15 @@ std::unique_ptr<Engine> Engine::Create(int device, int w, int h, std::string* er
     ok = false;
   e->scale_stride_ = (std::max(w, h) + 63) / 64 * 64;
   alloc(reinterpret_cast<void**>(&e->d_scales_), static_cast<size_t>(kNumSigmas) * 2 * e->scale_stride_ * 4);
-  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), e->nb_ * 4 + 16, hipHostMallocCoherent) !=
-                hipSuccess)
+  // (block maxima [nb_], 4 spare words, k_diffmap's tile maxima)
+  const size_t dm_groups = static_cast<size_t>((w + kDmTile - 1) / kDmTile) * ((h + kDmTile - 1) / kDmTile);
+  if (ok && hipHostMalloc(reinterpret_cast<void**>(&e->h_block_max_), (e->nb_ + 4 + dm_groups) * 4,
+                          hipHostMallocCoherent) != hipSuccess)
     ok = false;
   if (ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&e->m_block_max_), e->h_block_max_, 0) != hipSuccess)
     ok = false;
-  // k_diffmap's word, the last distance and its arrival counters
-  const size_t dm_groups = static_cast<size_t>((w + kDmTile - 1) / kDmTile) * ((h + kDmTile - 1) / kDmTile);
-  const size_t dm_bytes = 4 * (DmWgMaxOffset(dm_groups) + dm_groups + 4);
+  // k_diffmap's maxima words (the coder's skip test)
+  const size_t dm_bytes = 4 * kDmMaxWords;
   alloc(reinterpret_cast<void**>(&e->d_dmax_), dm_bytes);
   if (ok && hipMemsetAsync(e->d_dmax_, 0, dm_bytes, s) != hipSuccess) ok = false;
 
@@ -848,7 +849,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
     GZ_TIMED("opsin_mhic", k_opsin_mhic_stream<<<(strips * segs + 3) / 4, 256, 0, s>>>(
         d_px8_, d_ref_xyb_, w_, h_, strips, segs, rows, d_m0_, d_m1_, xyb_dbg, d_scales_,
-        scale_stride_));
+        scale_stride_, d_dmax_));
     if (xyb_dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;
   }
   if (dbg && !d2h(dbg->mhic0, d_m0_, 3 * n)) return false;
@@ -947,12 +948,9 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   {
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
-    const size_t dm_groups = static_cast<size_t>((w_ + kDmTile - 1) / kDmTile) * ((h_ + kDmTile - 1) / kDmTile);
-    float* wg_max = reinterpret_cast<float*>(d_dmax_ + DmWgMaxOffset(dm_groups));
-    GZ_TIMED("diffmap", (k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
-                             d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_, wg_max),
-                         k_distance<<<1, 256, 0, s>>>(wg_max, static_cast<int>(dm_groups), d_dmax_,
-                                                      m_block_max_ + nb_)));
+    GZ_TIMED("diffmap", k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
+                            d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_,
+                            m_block_max_ + nb_ + 4, d_dmax_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
   }
   ProfMark("compare_pass");
@@ -995,7 +993,7 @@ bool Engine::CompareEnqueue() {
     }
     GZ_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graph), s));
   }
-  // (the distance reaches h_block_max_[nb_] from k_diffmap_final itself)
+  // (k_diffmap's tile maxima reach h_block_max_ + nb_ + 4 themselves)
   return true;
 }
 
@@ -1006,7 +1004,13 @@ bool Engine::Sync() {
 }
 
 bool Engine::CompareFinish(float* distance, float* block_max) {
-  *distance = h_block_max_[nb_];
+  // ButteraugliScoreFromDiffmap's maximum from the tiles' (k_diffmap, mapped
+  // memory), folded as the device did: fmax from +0
+  const int groups = ((w_ + kDmTile - 1) / kDmTile) * ((h_ + kDmTile - 1) / kDmTile);
+  const float* wg = h_block_max_ + nb_ + 4;
+  float d = 0.0f;
+  for (int g = 0; g < groups; ++g) d = std::fmax(d, wg[g]);
+  *distance = d;
   if (block_max) {
     hipStream_t s = static_cast<hipStream_t>(stream_);
     GZ_HIP(hipSetDevice(device_));
@@ -1837,7 +1841,7 @@ bool Engine::JpegScanEnqueueRange(int ncomp, const int q[3][64], const JpegCodeT
   GZ_TIMED("jpeg_code", k_jpeg_code<<<groups, 256, 0, s>>>(d_cur_, qf, nb_, m0, m1, ncomp, dc,
                                                             static_cast<unsigned long long>(base),
                                                             pad_end ? 1 : 0, words, m_jhist_ + kJCodeHost, status,
-                                                            side, seam, jepoch_, d_dmax_ + kDistWord, skip_at));
+                                                            side, seam, jepoch_, d_dmax_, skip_at));
   jpart_[jslot_].base = base;
   jcode_groups_[jslot_] = groups;
   jcode_pad_[jslot_] = pad_end;

@@ -361,9 +361,9 @@ class Engine {
   size_t cbreq_cap_ = 0;
   int scale_stride_ = 0;
   // pinned host staging
-  float* h_block_max_ = nullptr;   // pinned: the block maxima on request; [nb_]: the distance (mapped)
+  float* h_block_max_ = nullptr;   // pinned: the block maxima on request; [nb_ + 4 ..]: k_diffmap's tile maxima (mapped)
   float* m_block_max_ = nullptr;
-  uint32_t* d_dmax_ = nullptr;      // k_diffmap: the last distance, arrival counters, per-workgroup maxima
+  uint32_t* d_dmax_ = nullptr;      // k_diffmap's kDmMaxWords maxima words (the coder's skip test)
   // device change order (allocated on first use): weight f32 | active i32 |
   // counts i32 | offsets i32 [nb + 1] | totals i32 [8] | arrival counters |
   // max_block_error f32 | last_indexes i32
