@@ -867,7 +867,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   }
   // (the search's passes compute the edge term in k_block_diff; the stage
   // dumps keep k_edge_map, whose output they read before block_diff runs)
-  const bool fuse_edge = !(dbg && dbg->edge);
+  static const bool fuse_env = !getenv("GZ_FUSE_EDGE") || atoi(getenv("GZ_FUSE_EDGE")) != 0;
+  const bool fuse_edge = fuse_env && !(dbg && dbg->edge);
   if (!fuse_edge)
     GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
