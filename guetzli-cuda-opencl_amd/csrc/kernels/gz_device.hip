@@ -938,6 +938,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     if (dbg_comb && !d2h(dbg->combined, dbg_comb, rn)) return false;
   } else {
     const MaskPlanes mkdc = MaskPlanesOf(d_mb_, n, true);
+    for (int c = 0; c < 3; ++c)  // (k_combine_channels indexes with compile-time steps)
+      if (mk.step[c] != kMaskStepSub[c] || mkdc.step[c] != kMaskStepSub[c]) return false;
     const size_t ldn = static_cast<size_t>((w_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]) *
                        ((h_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]);
     GZ_TIMED("combine_channels", k_combine_channels<<<PixGrid(rw_, rh_), 256, 0, s>>>(
