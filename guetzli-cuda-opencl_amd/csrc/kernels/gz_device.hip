@@ -951,7 +951,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   {
     float* dm = nullptr;
     if (dbg && dbg->distmap) dm = d_bl_;
-    GZ_TIMED("diffmap", k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), 256, 0, s>>>(
+    GZ_TIMED("diffmap", k_diffmap<<<dim3((w_ + kDmTile - 1) / kDmTile, (h_ + kDmTile - 1) / kDmTile), kDmThreads, 0, s>>>(
                             d_resval_, rw_, rh_, w_, h_, bw_, bh_, d_scales_, scale_stride_, dm, d_block_max_,
                             m_block_max_ + nb_ + 4, d_dmax_));
     if (dm && !d2h(dbg->distmap, dm, n)) return false;
