@@ -85,6 +85,20 @@ struct gz_comparator {
   std::vector<float> block_max;
   std::vector<int16_t> last;      // coefficients of the last compare (distmap())
   std::vector<uint8_t> last_rgb;  // ... or its sRGB pixels (gz_comparator_compare_rgb)
+  // ... or a 4:2:0 candidate (gz_comparator_compare_420): Y, Cb, Cr
+  // coefficients and the two factor-2 pixel planes
+  std::vector<int16_t> last420_coeffs[3];
+  std::vector<uint16_t> last420_planes[2];
+  bool Set420Again() {
+    return engine->Set420(last420_coeffs[0].data(), last420_coeffs[1].data(), last420_coeffs[2].data(),
+                          last420_planes[0].data(), last420_planes[1].data());
+  }
+  void ForgetLast() {
+    last.clear();
+    last_rgb.clear();
+    for (auto& v : last420_coeffs) v.clear();
+    for (auto& v : last420_planes) v.clear();
+  }
 };
 
 extern "C" {
@@ -164,8 +178,8 @@ static gz_status CompareImpl(gz_comparator* cmp, const int16_t* coeffs, gz::Comp
   cmp->block_max.resize(e.blocks());
   if (!e.UploadCoeffs(coeffs) || !e.Compare(&cmp->distance, cmp->block_max.data(), dbg))
     return SetError(GZ_ERR_DEVICE, "compare: " + e.error());
+  cmp->ForgetLast();
   cmp->last.assign(coeffs, coeffs + static_cast<size_t>(e.blocks()) * 192);
-  cmp->last_rgb.clear();
   if (distance) *distance = cmp->distance;
   return GZ_OK;
 }
@@ -176,8 +190,31 @@ gz_status gz_comparator_compare_rgb(gz_comparator* cmp, const uint8_t* rgb, floa
   cmp->block_max.resize(e.blocks());
   if (!e.SetCandidateRgb(rgb) || !e.Compare(&cmp->distance, cmp->block_max.data(), nullptr))
     return SetError(GZ_ERR_DEVICE, "compare_rgb: " + e.error());
+  cmp->ForgetLast();
   cmp->last_rgb.assign(rgb, rgb + static_cast<size_t>(3) * cmp->w * cmp->h);
-  cmp->last.clear();
+  if (distance) *distance = cmp->distance;
+  return GZ_OK;
+}
+
+gz_status gz_comparator_compare_420(gz_comparator* cmp, const int16_t* y, const int16_t* cb,
+                                    const int16_t* cr, const uint16_t* plane_cb, const uint16_t* plane_cr,
+                                    float* distance) {
+  if (!cmp || !y || !plane_cb || !plane_cr) return SetError(GZ_ERR_INVALID_ARG, "compare_420: bad argument");
+  gz::Engine& e = *cmp->engine;
+  const size_t per = static_cast<size_t>(e.blocks()) * 64;
+  const size_t cper = static_cast<size_t>((cmp->w + 15) / 16) * ((cmp->h + 15) / 16) * 64;
+  const size_t n = static_cast<size_t>(cmp->w) * cmp->h;
+  cmp->ForgetLast();
+  cmp->last420_coeffs[0].assign(y, y + per);
+  cmp->last420_coeffs[1] = cb ? std::vector<int16_t>(cb, cb + cper) : std::vector<int16_t>(cper, 0);
+  cmp->last420_coeffs[2] = cr ? std::vector<int16_t>(cr, cr + cper) : std::vector<int16_t>(cper, 0);
+  cmp->last420_planes[0].assign(plane_cb, plane_cb + n);
+  cmp->last420_planes[1].assign(plane_cr, plane_cr + n);
+  cmp->block_max.resize(e.blocks());
+  if (!cmp->Set420Again() || !e.Compare(&cmp->distance, cmp->block_max.data(), nullptr)) {
+    cmp->ForgetLast();
+    return SetError(GZ_ERR_DEVICE, "compare_420: " + e.error());
+  }
   if (distance) *distance = cmp->distance;
   return GZ_OK;
 }
@@ -206,9 +243,28 @@ gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs
   return CompareImpl(cmp, coeffs, &dbg, distance);
 }
 
+gz_status gz_comparator_compare_stages_production(gz_comparator* cmp, const int16_t* coeffs,
+                                                  gz_compare_stages* st, float* distance) {
+  gz::CompareDebug dbg;
+  dbg.production = true;
+  if (st) {
+    if (st->cand_linear || st->cand_xyb || st->block_ac_lf || st->mask || st->mask_dc || st->combined)
+      return SetError(GZ_ERR_INVALID_ARG,
+                      "compare_stages_production: only mhic0, mhic1, edge, block_dc, block_ac and distmap");
+    dbg.mhic0 = st->mhic0;
+    dbg.mhic1 = st->mhic1;
+    dbg.edge = st->edge;
+    dbg.block_dc = st->block_dc;
+    dbg.block_ac = st->block_ac;
+    dbg.distmap = st->distmap;
+  }
+  return CompareImpl(cmp, coeffs, &dbg, distance);
+}
+
 gz_status gz_comparator_distmap(gz_comparator* cmp, float* out) {
   if (!cmp || !out) return SetError(GZ_ERR_INVALID_ARG, "distmap: bad argument");
-  if (cmp->last.empty() && cmp->last_rgb.empty())
+  const bool is420 = !cmp->last420_planes[0].empty();
+  if (cmp->last.empty() && cmp->last_rgb.empty() && !is420)
     return SetError(GZ_ERR_INVALID_ARG, "distmap: no compare yet");
   gz::Engine& e = *cmp->engine;
   // the pass again on the same candidate, with the map read back (the
@@ -216,7 +272,9 @@ gz_status gz_comparator_distmap(gz_comparator* cmp, float* out) {
   gz::CompareDebug dbg;
   dbg.distmap = out;
   float d = 0.0f;
-  const bool up = cmp->last.empty() ? e.SetCandidateRgb(cmp->last_rgb.data()) : e.UploadCoeffs(cmp->last.data());
+  const bool up = is420 ? cmp->Set420Again()
+                  : cmp->last.empty() ? e.SetCandidateRgb(cmp->last_rgb.data())
+                                      : e.UploadCoeffs(cmp->last.data());
   if (!up || !e.Compare(&d, nullptr, &dbg)) return SetError(GZ_ERR_DEVICE, "distmap: " + e.error());
   return GZ_OK;
 }

@@ -1491,9 +1491,11 @@ class Processor {
 
  private:
   bool Fail(std::string* err) {
-    if (err) *err = cmp_->error();
+    if (err) *err = internal_err_.empty() ? cmp_->error() : internal_err_;
     return false;
   }
+  // an inconsistency found by the loop itself, not by the comparator
+  std::string internal_err_;
   void OutputJpeg(const JpegData& jpg, std::string* out) {
     const auto t0 = Clock::now();
     out->clear();
@@ -1908,7 +1910,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // the order open
       auto fetch_exact = [&]() -> bool {
         if (!cmp_->DeviceOrderEntries(&global_order)) return false;
-        if (global_order.size() != frame_n) return false;
+        if (global_order.size() != frame_n) {
+          internal_err_ = "device order: entry count mismatch";
+          return false;
+        }
         sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
         res_->detail["backend_order_fetches"] += 1;
         return true;
@@ -2288,10 +2293,12 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         auto tail_ready = [&](size_t s) -> bool {
           if (!tail_exact) {
             if (s < win_base + win_ok) return true;
-            if (win_ok == win.size() && !win_last && s == win_base + win_ok) {
+            // (no window at all -- the selection's candidates overflowed, or
+            // its prefix was open -- goes straight to the exact order)
+            if (!win.empty() && win_ok == win.size() && !win_last && s == win_base + win_ok) {
               // the window ran out without a tie: the next one from rank s
               Engine::OrderSelection next;
-              const size_t want = std::min<size_t>(8192, 2 * win.size());
+              const size_t want = std::min<size_t>(8192, std::max<size_t>(512, 2 * win.size()));
               if (!cmp_->DeviceSelectWindow(s, want, direction, &next)) return false;
               res_->detail["backend_tail_windows"] += 1;
               if (!next.open && !next.window_overflow) {
@@ -2306,6 +2313,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             if (bulk) sorter->SetPrefix(bulk);
             tail_exact = true;
             res_->detail["backend_tail_exact"] += 1;
+            if (!bulk && win.empty()) res_->detail["backend_tail_exact_nobulk"] += 1;
           }
           if (s >= sorter->sorted()) {
             const auto ts = Clock::now();

@@ -868,14 +868,17 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // (the search's passes compute the edge term in k_block_diff; the stage
   // dumps keep k_edge_map, whose output they read before block_diff runs)
   static const bool fuse_env = !getenv("GZ_FUSE_EDGE") || atoi(getenv("GZ_FUSE_EDGE")) != 0;
-  const bool fuse_edge = fuse_env && !(dbg && dbg->edge);
+  const bool prod = dbg && dbg->production;
+  const bool fuse_edge = fuse_env && !(dbg && dbg->edge && !prod);
   if (!fuse_edge)
     GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
-  if (dbg && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
+  if (dbg && !fuse_edge && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   // S6: block diff
   GZ_TIMED("block_diff", k_block_diff<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), kBdThreads, 0, s>>>(
       d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_, fuse_edge ? d_bl_ : nullptr,
       fuse_edge ? d_bl_ + 3 * n : nullptr, d_edge_));
+  // (the fused edge term is in d_edge_ once k_block_diff has run)
+  if (dbg && fuse_edge && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;
   // S7 + S12: the six sigma-14 blurs (low-frequency edge term, m0 / m1) and
@@ -885,10 +888,10 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   // (raw blurred mask planes for the stage dumps of the masks and of the
   // combined value; the search's passes apply the mask LUTs per sample in
   // the vertical pass and combine without them)
-  const bool full_mask = dbg && (dbg->mask || dbg->mask_dc || dbg->combined);
+  const bool full_mask = dbg && !prod && (dbg->mask || dbg->mask_dc || dbg->combined);
   // EdgeDetectorLowFreq's term is fused into k_combine_channels unless a
   // stage dump wants the AC values with it, or k_combine runs
-  const bool fuse_lf = !full_mask && !(dbg && dbg->block_ac_lf);
+  const bool fuse_lf = !full_mask && !(dbg && dbg->block_ac_lf && !prod);
   {
     const int st = HostTables().blur[kSigLowFreq].step;
     const size_t dn = static_cast<size_t>((w_ + st - 1) / st) * ((h_ + st - 1) / st);
@@ -922,9 +925,9 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     if (!fuse_lf)
       GZ_TIMED("low_freq", k_low_freq<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * dn, w_, h_, rw_, d_ac_));
   }
-  if (dbg && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
+  if (dbg && !prod && !d2h(dbg->block_ac_lf, d_ac_, 3 * rn)) return false;
   MaskPlanes mk = MaskPlanesOf(d_ma_, n, !full_mask);
-  if (dbg && (dbg->mask || dbg->mask_dc)) {
+  if (dbg && full_mask && (dbg->mask || dbg->mask_dc)) {
     GZ_TIMED("mask_full_dbg", k_mask_full<<<PixGrid(w_, h_), 256, 0, s>>>(mk, w_, h_, d_mb_, d_tmp_));
     if (!d2h(dbg->mask, d_mb_, 3 * n)) return false;
     if (!d2h(dbg->mask_dc, d_tmp_, 3 * n)) return false;
@@ -939,7 +942,8 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   } else {
     const MaskPlanes mkdc = MaskPlanesOf(d_mb_, n, true);
     for (int c = 0; c < 3; ++c)  // (k_combine_channels indexes with compile-time steps)
-      if (mk.step[c] != kMaskStepSub[c] || mkdc.step[c] != kMaskStepSub[c]) return false;
+      if (mk.step[c] != kMaskStepSub[c] || mkdc.step[c] != kMaskStepSub[c])
+        return Fail("combine_channels: mask plane steps", hipErrorInvalidValue);
     const size_t ldn = static_cast<size_t>((w_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]) *
                        ((h_ + kBlurGeomStep[kSigLowFreq] - 1) / kBlurGeomStep[kSigLowFreq]);
     GZ_TIMED("combine_channels", k_combine_channels<<<PixGrid(rw_, rh_), 256, 0, s>>>(
@@ -1666,7 +1670,10 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   out->open = host->open != 0;
   out->applied = has_prefix && apply && !out->open;
   out->window_n = static_cast<size_t>(host->cand_n);
-  out->window_overflow = host->overflow != 0;
+  // (GZ_SEL_OVERFLOW=1: every window reported overflowed -- tests of the
+  // back end's path without a window, the bulk prefix applied or not)
+  static const int force_overflow = getenv("GZ_SEL_OVERFLOW") ? atoi(getenv("GZ_SEL_OVERFLOW")) : 0;
+  out->window_overflow = host->overflow != 0 || force_overflow;
   out->window_last = host->window_last != 0;
   if (out->applied) out->cnt.assign(h_bulk_, h_bulk_ + nb_);
   else out->cnt.clear();

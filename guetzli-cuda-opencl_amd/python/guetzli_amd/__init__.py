@@ -70,7 +70,8 @@ EXPORTED_SYMBOLS = (
     "gz_last_error", "gz_build_info", "gz_device_count", "gz_params_init",
     "gz_butteraugli_score_for_quality", "gz_free", "gz_process_rgb", "gz_process_rgb_device",
     "gz_comparator_create", "gz_comparator_destroy", "gz_comparator_compare",
-    "gz_comparator_compare_stages", "gz_comparator_block_max", "gz_comparator_distance_ok",
+    "gz_comparator_compare_stages", "gz_comparator_compare_stages_production", "gz_comparator_compare_420",
+    "gz_comparator_block_max", "gz_comparator_distance_ok",
     "gz_comparator_score_output_size", "gz_comparator_start_block_comparisons",
     "gz_comparator_block_zeroing_orders", "gz_synthetic_frame", "gz_rgb_to_coeffs",
     "gz_block_error_adjustment_weights", "gz_engine_pool_trim", "gz_engine_pool_idle_bytes",
@@ -133,6 +134,11 @@ def lib():
     L.gz_comparator_compare.restype = i32
     L.gz_comparator_compare_stages.argtypes = [vp, vp, ctypes.POINTER(_Stages), ctypes.POINTER(f32)]
     L.gz_comparator_compare_stages.restype = i32
+    L.gz_comparator_compare_stages_production.argtypes = [vp, vp, ctypes.POINTER(_Stages),
+                                                          ctypes.POINTER(f32)]
+    L.gz_comparator_compare_stages_production.restype = i32
+    L.gz_comparator_compare_420.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.POINTER(f32)]
+    L.gz_comparator_compare_420.restype = i32
     L.gz_comparator_distmap.argtypes = [vp, vp]
     L.gz_comparator_distmap.restype = i32
     L.gz_comparator_compare_blocks.argtypes = [vp, i32, vp, vp, vp]
@@ -636,6 +642,42 @@ class ButteraugliComparator:
         _check(lib().gz_comparator_compare_stages(self._h, _ptr(self._coeffs(coeffs)),
                                                   ctypes.byref(st), ctypes.byref(d)),
                "compare_stages")
+        arrs["distance"] = d.value
+        return arrs
+
+    def compare_420(self, y, plane_cb, plane_cr, cb=None, cr=None):
+        """Compare of a 4:2:0 candidate: Y coefficients and the factor-2
+        chroma pixel planes (uint16, h x w, wrapping state)."""
+        n = self.width * self.height
+        yy = np.ascontiguousarray(y, dtype=np.int16).reshape(-1)
+        pcb = np.ascontiguousarray(plane_cb, dtype=np.uint16).reshape(-1)
+        pcr = np.ascontiguousarray(plane_cr, dtype=np.uint16).reshape(-1)
+        cper = ((self.width + 15) // 16) * ((self.height + 15) // 16) * 64
+        if yy.size != 64 * ((self.width + 7) // 8) * ((self.height + 7) // 8) or pcb.size != n or pcr.size != n:
+            raise GuetzliError(1, "compare_420: shapes")
+        cbs = [None if a is None else np.ascontiguousarray(a, dtype=np.int16).reshape(-1) for a in (cb, cr)]
+        if any(a is not None and a.size != cper for a in cbs):
+            raise GuetzliError(1, "compare_420: chroma coefficient shapes")
+        d = ctypes.c_float()
+        _check(lib().gz_comparator_compare_420(self._h, _ptr(yy), None if cbs[0] is None else _ptr(cbs[0]),
+                                               None if cbs[1] is None else _ptr(cbs[1]), _ptr(pcb), _ptr(pcr),
+                                               ctypes.byref(d)), "compare_420")
+        return d.value
+
+    def compare_stages_production(self, coeffs):
+        """Compare with the planes the search's own (fused) kernels leave in
+        HBM returned: mhic0, mhic1, edge (k_block_diff's fused corner term),
+        block_dc, block_ac (before the low-frequency term) and distmap."""
+        n = self.width * self.height
+        rn = ((self.width + 2) // 3) * ((self.height + 2) // 3)
+        sizes = {"mhic0": 3 * n, "mhic1": 3 * n, "edge": 3 * rn, "block_dc": 3 * rn,
+                 "block_ac": 3 * rn, "distmap": n}
+        arrs = {k: np.zeros(v, dtype=np.float32) for k, v in sizes.items()}
+        st = _Stages(**{k: a.ctypes.data for k, a in arrs.items()})
+        d = ctypes.c_float()
+        _check(lib().gz_comparator_compare_stages_production(self._h, _ptr(self._coeffs(coeffs)),
+                                                             ctypes.byref(st), ctypes.byref(d)),
+               "compare_stages_production")
         arrs["distance"] = d.value
         return arrs
 

@@ -200,9 +200,27 @@ gz_status gz_comparator_compare(gz_comparator* cmp, const int16_t* coeffs, float
  * entry for images whose pixels are not a function of their coefficients
  * alone (4:2:0: the subsampled components' upsampled pixels are state). */
 gz_status gz_comparator_compare_rgb(gz_comparator* cmp, const uint8_t* rgb, float* distance);
+/* Compare of a 4:2:0 candidate (OutputImage with factor-2 chroma,
+ * output_image.cc:642-716): Y coefficients ([blocks][64]), Cb / Cr
+ * coefficients ([ceil(w/16)*ceil(h/16)][64] each; NULL = zeros -- the
+ * Compare pass reads the chroma from the planes) and the factor-2 components'
+ * 16-bit pixel state (w*h each, wrapping: ToPixels' byte is
+ * ((p + 8 - (x & 1)) >> 4) & 0xff, output_image.cc:83). */
+gz_status gz_comparator_compare_420(gz_comparator* cmp, const int16_t* y, const int16_t* cb,
+                                    const int16_t* cr, const uint16_t* plane_cb, const uint16_t* plane_cr,
+                                    float* distance);
 /* Same, with stage dumps. */
 gz_status gz_comparator_compare_stages(gz_comparator* cmp, const int16_t* coeffs,
                                        gz_compare_stages* stages, float* distance);
+/* Same, dumped from the search's own (fused) kernel variants instead of the
+ * stand-alone dump kernels -- the corner edge term as k_block_diff leaves it,
+ * block_ac before the low-frequency term, the distance map after the fused
+ * combine (low-frequency term, subsampled B mask, LUT'd mask samples).  Only
+ * mhic0, mhic1, edge, block_dc, block_ac and distmap may be non-NULL
+ * (GZ_ERR_INVALID_ARG otherwise).  Parity evidence for the kernels the search
+ * runs (clbutter_comparator.cpp:1387-1417). */
+gz_status gz_comparator_compare_stages_production(gz_comparator* cmp, const int16_t* coeffs,
+                                                  gz_compare_stages* stages, float* distance);
 /* EncodeRGBToJpeg's q=1 coefficients of the comparator's reference image
  * ([3][blocks][64] int16, natural order) computed on the device: YUV16 +
  * integer FDCT + q=1 quantizer (guetzli/jpeg_data_encoder.cc:66-136,

@@ -65,6 +65,92 @@ def test_compare_stages_bit_exact(gz, case):
     assert bits_equal(cmp.block_max(), bm)
 
 
+PROD_STAGES = ["mhic0", "mhic1", "edge", "block_dc", "block_ac", "distmap"]
+
+
+@pytest.mark.parametrize("case", fixture_cases())
+def test_production_stages_bit_exact(gz, case):
+    """The planes of the search's own kernel variants (k_block_diff with the
+    corner edge term fused in, k_combine_channels with the low-frequency term
+    and the subsampled B mask, the LUT epilogue of the vertical blur) against
+    the reference's stage dumps -- not the stand-alone dump kernels that
+    compare_stages switches to."""
+    F = Fixture(case)
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    st = cmp.compare_stages_production(F.i16("cand_coeffs.i16"))
+    bad = []
+    for name in PROD_STAGES:
+        ref = F.f32(FIXTURE_FILE.get(name, name + ".f32"))
+        if not bits_equal(st[name], ref):
+            bad.append("%s: %s" % (name, mismatch(st[name], ref)))
+    assert not bad, "; ".join(bad)
+    assert np.float32(st["distance"]) == np.float32(F.meta["distance"])
+    # the search's plain (graph-launched) pass and distmap() agree with it
+    assert np.float32(cmp.compare(F.i16("cand_coeffs.i16"))) == np.float32(F.meta["distance"])
+    assert bits_equal(cmp.distmap(), st["distmap"])
+
+
+def test_production_stages_reject_dump_only_planes(gz):
+    """Planes only the dump kernels produce are refused, not silently zero."""
+    F = Fixture(fixture_cases()[0])
+    cmp = gz.ButteraugliComparator(F.w, F.h, F.rgb(), F.target)
+    n = F.w * F.h
+    arr = np.zeros(3 * n, np.float32)
+    st = gz._Stages(mask=arr.ctypes.data)
+    rc = gz.lib().gz_comparator_compare_stages_production(cmp._h, gz._ptr(F.i16("cand_coeffs.i16")),
+                                                           gz.ctypes.byref(st), None)
+    assert rc != 0 and "only mhic0" in gz.lib().gz_last_error().decode()
+
+
+def test_420_chroma_planes_wrap_to_pixel_bytes(gz):
+    """k_coeffs_to_srgb8's 4:2:0 input: the factor-2 chroma planes are 16-bit
+    state that wraps (the inverse upsampler can drive a pixel below 0 or past
+    4095), and ToPixels keeps the low byte of (p + 8 - (x & 1)) >> 4
+    (output_image.cc:83, a uint8_t cast).  Planes drawn over all 65536 values
+    (both wrap directions, both x parities) must give the candidate the
+    oracle forms from the same bytes -- compared as whole distance maps."""
+    import ctypes
+    L = oracle()
+    L.gzo_ycbcr_to_rgb.argtypes = [ctypes.c_void_p]
+    L.gzo_ycbcr_to_rgb.restype = None
+    w, h = 96, 64
+    rng = np.random.default_rng(42)
+    rgb = gz.synthetic_frame(3, w, h)
+    bw, bh = w // 8, h // 8
+    y = np.zeros((bh * bw, 64), np.int16)
+    y[:, 0] = rng.integers(-600, 600, size=bh * bw)
+    y[:, 1:10] = rng.integers(-40, 40, size=(bh * bw, 9))
+    planes = rng.integers(0, 65536, size=(2, h, w)).astype(np.uint16)
+    # make sure the wrap edges are present: just below 0, around 4095/4096
+    planes[0, 0, :8] = [0xFFF0, 0xFFF7, 0xFFF8, 0xFFFF, 4087, 4088, 4095, 4104]
+    planes[1, 1, :8] = [4104, 4095, 4088, 4087, 0xFFFF, 0xFFF8, 0xFFF7, 0xFFF0]
+    xs = np.arange(w)[None, :]
+    byte = ((planes.astype(np.int64) + 8 - (xs & 1)) >> 4) & 0xff
+    assert (byte[0, 0, :8] == [255, 255, 0, 0, 255, 255, 0, 0]).all()  # 4095 -> 255, 4096 -> 0 (wrapped)
+    ypix = np.zeros((h, w), np.uint8)
+    for b in range(bh * bw):
+        out = np.zeros(64, np.uint8)
+        L.gzo_block_idct(y[b], out)
+        by, bx = divmod(b, bw)
+        ypix[8 * by:8 * by + 8, 8 * bx:8 * bx + 8] = out.reshape(8, 8)
+    exp = np.stack([ypix, byte[0], byte[1]], axis=-1).astype(np.uint8).copy()
+    for p in range(w * h):
+        L.gzo_ycbcr_to_rgb(exp.ctypes.data + 3 * p)
+    cmp = gz.ButteraugliComparator(w, h, rgb, 1.0)
+    d420 = cmp.compare_420(y, planes[0], planes[1])
+    bm420 = cmp.block_max()
+    dm420 = cmp.distmap()
+    dr = ctypes.c_float()
+    assert gz.lib().gz_comparator_compare_rgb(cmp._h, gz._ptr(exp.reshape(-1)), ctypes.byref(dr)) == 0
+    assert np.float32(d420) == np.float32(dr.value)
+    assert bits_equal(bm420, cmp.block_max())
+    assert bits_equal(dm420, cmp.distmap()), mismatch(dm420, cmp.distmap())
+    # a saturating byte (what a packed saturating store would give) is a
+    # different candidate: the test can tell the two semantics apart
+    sat = np.clip((planes.astype(np.int64) + 8 - (xs & 1)) >> 4, 0, 255)
+    assert (sat != byte).mean() > 0.5
+
+
 @pytest.mark.parametrize("case", fixture_cases())
 def test_block_mask_scale_bit_exact(gz, case):
     F = Fixture(case)
@@ -316,6 +402,11 @@ def test_compare_matches_oracle_on_synthetic(gz, w, h, seed):
     d = L.gzo_compare(w, h, rgb.ravel(), cand, dm)
     assert bits_equal(st["distmap"], dm), mismatch(st["distmap"], dm)
     assert np.float32(st["distance"]) == np.float32(d)
+    # the production (fused) variants: every distance-map pixel
+    pr = cmp.compare_stages_production(cand)
+    assert bits_equal(pr["distmap"], dm), mismatch(pr["distmap"], dm)
+    for k in ("edge", "block_dc", "block_ac"):
+        assert bits_equal(pr[k], st[k]), "%s: %s" % (k, mismatch(pr[k], st[k]))
 
 
 @pytest.mark.parametrize("w,h,seed", [(256, 256, 7), (333, 197, 8), (517, 389, 4), (700, 301, 5),
@@ -490,13 +581,20 @@ rgb = gz.synthetic_frame(e["seed"], e["w"], e["h"])
 data, stats = gz.process(rgb, e["w"], e["h"], gz.Params.for_quality(e["quality"]), return_stats=True)
 d = gz.last_process_detail()
 print(json.dumps({"sha": hashlib.sha256(data).hexdigest(), "iters": stats.iterations,
-                  "undone": d.get("backend_spec_undone", 0), "codes": d.get("backend_entropy_codes", 0)}))
+                  "undone": d.get("backend_spec_undone", 0), "codes": d.get("backend_entropy_codes", 0),
+                  "detail": {k: v for k, v in d.items() if k.startswith("backend_") and not k.endswith("_s")}}))
 """
+
+# the counter each knob must move (the forced path really ran)
+_VARIANT_EVIDENCE = {"GZ_TAIL_WINDOW": ("backend_tail_windows", "backend_tail_exact"),
+                     "GZ_SELECT_OPEN": ("backend_select_open",),
+                     "GZ_SEL_OVERFLOW": ("backend_tail_exact_nobulk",)}
 
 
 @pytest.mark.parametrize("env", [{"GZ_REPLAY_DIV": "1000000"}, {"GZ_SPEC_DECADES": "1"},
                                  {"GZ_SPEC_DECADES": "32", "GZ_SPIN_US": "0"},
-                                 {"GZ_TAIL_WINDOW": "16"}, {"GZ_SELECT_OPEN": "1"}])
+                                 {"GZ_TAIL_WINDOW": "16"}, {"GZ_SELECT_OPEN": "1"},
+                                 {"GZ_SEL_OVERFLOW": "1"}])
 def test_backend_variants_keep_known_answer(env):
     """Back-end variants that must not change the bytes (each in its own
     process: the knobs are read once).  GZ_REPLAY_DIV=1e6: every journal
@@ -507,7 +605,11 @@ def test_backend_variants_keep_known_answer(env):
     selection's tail window runs out early, the tail continues in
     std::sort's exact order from there; GZ_SELECT_OPEN=1: every bulk prefix
     reported open (as when its last key is shared by several blocks), so
-    the prefix is taken from std::sort's exact order on the host."""
+    the prefix is taken from std::sort's exact order on the host;
+    GZ_SEL_OVERFLOW=1: every selection's window overflows, so the tail has no
+    window at all -- including iterations without a bulk prefix, whose empty
+    window used to ask the device for a zero-entry window.  The
+    knob's counter must move, so the forced path is known to have run."""
     import subprocess
     import sys
     name = "synth_640x360_s3_q95"
@@ -518,6 +620,11 @@ def test_backend_variants_keep_known_answer(env):
     assert res.returncode == 0, res.stderr[-2000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["sha"] == e["sha256"] and out["iters"] == e["iters"], out
+    for knob, counters in _VARIANT_EVIDENCE.items():
+        if knob in env:
+            assert any(out["detail"].get(c, 0) > 0 for c in counters), (knob, out["detail"])
+    if "GZ_SPEC_DECADES" in env:
+        assert out["codes"] > 0, out
 
 
 _ZIGZAG = [0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24,
@@ -559,3 +666,14 @@ def test_compare_stages_at_frame_size(gz, name):
            if hashlib.sha256(np.ascontiguousarray(st[k], np.float32).tobytes()).hexdigest() != e["sha256"][k]]
     assert not bad, "stages differing from the reference at %dx%d: %s" % (w, h, bad)
     assert np.float32(st["distance"]) == np.float32(e["distance"])
+    # the kernels the search runs (fused edge term, fused low-frequency term,
+    # subsampled B mask, LUT epilogue), per pixel at the same frame size
+    del st
+    pr = cmp.compare_stages_production(cand)
+    bad = [k for k in PROD_STAGES
+           if hashlib.sha256(np.ascontiguousarray(pr[k], np.float32).tobytes()).hexdigest() != e["sha256"][k]]
+    assert not bad, "production stages differing from the reference at %dx%d: %s" % (w, h, bad)
+    assert np.float32(pr["distance"]) == np.float32(e["distance"])
+    assert np.float32(cmp.compare(cand)) == np.float32(e["distance"])
+    dm = cmp.distmap()
+    assert hashlib.sha256(np.ascontiguousarray(dm, np.float32).tobytes()).hexdigest() == e["sha256"]["distmap"]
