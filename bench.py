@@ -382,6 +382,36 @@ def cpu_baseline(width, height, quality, processes=8):
                 reference_bytes_match_manifest="%d/%d" % (matched, cores))
 
 
+def strip_collectives(gz, dist, group, rank, dev):
+    """The strips' exchange for ranks 0-3: the library's own RCCL
+    communicator (gz_rccl_create: all-gathers on its own stream, no Python
+    in the exchange) when every rank can load RCCL and the four ranks sit on
+    four different GPUs (RCCL refuses two ranks on one device -- the
+    one-GPU test runs four ranks on cuda:0), else torch.distributed's
+    collectives through the ctypes callback.  The decision is taken
+    together, so no rank waits in ncclCommInitRank for one that fell back."""
+    import torch
+    ok = 0
+    try:
+        ok = 1 if gz.rccl_library() else 0
+    except Exception:
+        ok = 0
+    tdev = "cuda:%d" % dev
+    # (the decision's own exchange: on the device for the nccl backend, on
+    # the host for gloo -- the one-GPU test's four ranks)
+    cdev = tdev if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([ok, dev], dtype=torch.int64, device=cdev)
+    got = [torch.zeros_like(t) for _ in range(4)]
+    dist.all_gather(got, t, group=group)
+    oks = [int(g[0].item()) for g in got]
+    devs = [int(g[1].item()) for g in got]
+    if all(oks) and len(set(devs)) == 4 and os.environ.get("GZ_STRIP_TORCH_EXCHANGE") != "1":
+        obj = [gz.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return gz.Collectives.from_rccl(dev, rank, 4, obj[0]), "RCCL, library communicator"
+    return gz.Collectives.from_torch(dist, tdev, group=group), "torch.distributed exchange"
+
+
 def large_frame(gz, dist, world, rank, dev, w=8192, h=8192, q=84, seed=0):
     """BASELINE configs[4] after the timed region: one synthetic 8192x8192
     frame at q=84 (seed 0, whose reference bytes are committed).  With N >= 4
@@ -402,7 +432,7 @@ def large_frame(gz, dist, world, rank, dev, w=8192, h=8192, q=84, seed=0):
         group = dist.new_group([0, 1, 2, 3])
         if rank >= 4:
             return None
-        coll = gz.Collectives.from_torch(dist, "cuda:%d" % dev, group=group)
+        coll, exchange = strip_collectives(gz, dist, group, rank, dev)
 
         def run():
             return gz.process_strips(rgb, w, h, coll, params, device=dev)
@@ -419,12 +449,13 @@ def large_frame(gz, dist, world, rank, dev, w=8192, h=8192, q=84, seed=0):
     data = run()
     elapsed = time.perf_counter() - t0
     if strips:
+        coll.close()
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         elapsed = float(t.item())
     sha = hashlib.sha256(data).hexdigest()
     return {"config": "BASELINE configs[4]: synthetic %dx%d q%d (seed %d)" % (w, h, q, seed),
-            "mode": "4 row strips + halo over GPUs 0-3 (RCCL)" if strips else "one engine, 1 GPU",
+            "mode": "4 row strips + halo over GPUs 0-3 (%s)" % exchange if strips else "one engine, 1 GPU",
             "gpus": 4 if strips else 1, "seconds": round(elapsed, 3),
             "Mpixels_per_s": round(w * h / elapsed / 1e6, 3), "bytes": len(data),
             "bit_exact": bool(kn and kn[0] == sha), "against": "reference guetzli --c sha256"}

@@ -700,6 +700,12 @@ gz_status gz_rccl_create(int device, int rank, int world, const uint8_t id[128],
   return GZ_OK;
 }
 
+const char* gz_rccl_library(void) {
+  static thread_local std::string path;
+  path = gz::RcclLibraryPath();
+  return path.c_str();
+}
+
 void gz_rccl_destroy(gz_rccl* comm) { gz::RcclDestroy(reinterpret_cast<gz::RcclComm*>(comm)); }
 
 }  // extern "C"

@@ -59,9 +59,16 @@ bool StagedAllGather::Run(const void* send, size_t bytes, void* recv) {
 
 namespace {
 
-// The few RCCL entry points used, resolved once from librccl (ROCm's
-// /opt/rocm/lib).  The types are RCCL's (rccl.h) restated: opaque handles,
-// an int result, the 128-byte id.
+// The few RCCL entry points used, resolved once from librccl.  The types are
+// RCCL's (rccl.h) restated: opaque handles, an int result, the 128-byte id.
+//
+// Which librccl: the one beside the HIP runtime this process already uses.
+// The library's own libamdhip64.so.7 dependency binds to whatever runtime of
+// that soname is mapped first -- in a process that imported torch, the one
+// torch bundles (torch/lib).  The system RCCL (/opt/rocm) against that
+// runtime fails in ncclCommInitRank (hipGetDeviceCount), so the RCCL built
+// with the mapped runtime -- torch's own librccl.so beside it, or ROCm's in
+// /opt/rocm/lib for a plain C++ caller -- is tried first.
 struct RcclApi {
   using Comm = void*;
   struct UniqueId {
@@ -73,6 +80,7 @@ struct RcclApi {
   int (*CommDestroy)(Comm) = nullptr;
   const char* (*GetErrorString)(int) = nullptr;
   std::string err;
+  std::string path;  // the librccl loaded
   bool ok = false;
 };
 constexpr int kRcclUint8 = 1;  // ncclUint8 (ncclDataType_t)
@@ -81,11 +89,28 @@ const RcclApi& Api() {
   static RcclApi api;
   static std::once_flag once;
   std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    void* h = nullptr;
+    std::string tried;
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void*>(&hipGetDeviceCount), &info) && info.dli_fname) {
+      std::string dir = info.dli_fname;
+      const size_t slash = dir.rfind('/');
+      dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
+      for (const char* name : {"/librccl.so.1", "/librccl.so"}) {
+        const std::string path = dir + name;
+        h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+          api.path = path;
+          break;
+        }
+        tried += path + " ";
+      }
+    }
+    if (!h && (h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL))) api.path = "librccl.so.1";
+    if (!h && (h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL))) api.path = "/opt/rocm/lib/librccl.so.1";
     if (!h) {
       const char* e = dlerror();
-      api.err = std::string("librccl not loadable: ") + (e ? e : "?");
+      api.err = std::string("librccl not loadable (") + tried + "librccl.so.1): " + (e ? e : "?");
       return;
     }
     api.GetUniqueId = reinterpret_cast<decltype(api.GetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
@@ -108,7 +133,11 @@ std::string RcclMessage(const char* what, int r) {
 class RcclTransport : public StagedAllGather::Transport {
  public:
   RcclTransport(int device, RcclApi::Comm comm, hipStream_t s) : device_(device), comm_(comm), s_(s) {}
-  bool DeviceAlloc(size_t bytes, void** p) override { return Hip(hipMalloc(p, bytes), "hipMalloc"); }
+  // (staging buffers on the communicator's device, whatever device the
+  // calling thread had current)
+  bool DeviceAlloc(size_t bytes, void** p) override {
+    return Hip(hipSetDevice(device_), "hipSetDevice") && Hip(hipMalloc(p, bytes), "hipMalloc");
+  }
   void DeviceFree(void* p) override { (void)hipFree(p); }
   bool HostAlloc(size_t bytes, void** p) override { return Hip(hipHostMalloc(p, bytes), "hipHostMalloc"); }
   void HostFree(void* p) override { (void)hipHostFree(p); }
@@ -217,5 +246,7 @@ int RcclAllGather(void* ctx, const void* send, size_t bytes, void* recv) {
 }
 
 const std::string& RcclError(const RcclComm* c) { return c->err; }
+
+const std::string& RcclLibraryPath() { return Api().path; }
 
 }  // namespace gz

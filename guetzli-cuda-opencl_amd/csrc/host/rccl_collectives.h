@@ -84,5 +84,7 @@ RcclComm* RcclCreate(int device, int rank, int world, const uint8_t id[kRcclIdBy
 void RcclDestroy(RcclComm* c);
 int RcclAllGather(void* ctx, const void* send, size_t bytes, void* recv);
 const std::string& RcclError(const RcclComm* c);
+// The librccl the communicators use (loaded on first use; empty if none).
+const std::string& RcclLibraryPath();
 
 }  // namespace gz

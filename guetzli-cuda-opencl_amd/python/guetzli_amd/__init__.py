@@ -81,6 +81,7 @@ EXPORTED_SYMBOLS = (
     "gz_collectives_selftest", "gz_process_jpeg", "gz_jpeg_decode", "gz_comparator_distmap",
     "gz_comparator_compare_blocks", "gz_png_decode", "gz_comparator_compare_rgb",
     "gz_comparator_compare_blocks_rgb", "gz_rccl_unique_id", "gz_rccl_create", "gz_rccl_destroy",
+    "gz_rccl_library",
 )
 
 _lib = None
@@ -182,6 +183,8 @@ def lib():
                                  ctypes.POINTER(_Collectives)]
     L.gz_rccl_destroy.argtypes = [vp]
     L.gz_rccl_destroy.restype = None
+    L.gz_rccl_library.argtypes = []
+    L.gz_rccl_library.restype = ctypes.c_char_p
     L.gz_profile_enable.argtypes = [i32]
     L.gz_profile_get.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long),
                                  ctypes.POINTER(ctypes.c_double)]
@@ -507,6 +510,11 @@ class Collectives:
 
     def selftest(self):
         _check(lib().gz_collectives_selftest(ctypes.byref(self._c)), "collectives_selftest")
+
+
+def rccl_library():
+    """Path of the librccl the library's communicators use (gz_rccl_library)."""
+    return lib().gz_rccl_library().decode()
 
 
 def rccl_unique_id():

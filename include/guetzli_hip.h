@@ -178,13 +178,18 @@ gz_status gz_collectives_selftest(const gz_collectives* coll);
  * hands the 128 bytes to the others by its own means (MPI, a file, a
  * socket); every rank then calls gz_rccl_create (ncclCommInitRank: returns
  * when all have), which fills *coll for gz_process_rgb_strips.  RCCL is
- * loaded on first use (librccl.so.1).  gz_rccl_destroy after the last
- * encode that uses *coll. */
+ * loaded on first use: the librccl beside the HIP runtime the process has
+ * mapped (torch's own in a process that imported torch, else ROCm's), then
+ * librccl.so.1 from the search path.  gz_rccl_destroy after the last encode
+ * that uses *coll. */
 typedef struct gz_rccl gz_rccl;
 gz_status gz_rccl_unique_id(uint8_t id[128]);
 gz_status gz_rccl_create(int device, int rank, int world, const uint8_t id[128], gz_rccl** out,
                          gz_collectives* coll);
 void gz_rccl_destroy(gz_rccl* comm);
+/* Path of the librccl loaded (empty before the first gz_rccl_* call or if
+ * none could be loaded). */
+const char* gz_rccl_library(void);
 
 /* ---- comparator (guetzli::ButteraugliComparator) ---------------------- */
 /* ButteraugliComparator(w, h, rgb, target, stats) ctor

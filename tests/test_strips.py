@@ -256,6 +256,52 @@ sys.exit(0 if got == want else 3)
 """
 
 
+_RCCL_TORCH_CHILD = r"""
+import hashlib, os, sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import guetzli_amd as gz
+w, h, quality, path, want = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], sys.argv[6]
+# torch's HIP runtime initialised first, as in bench.py's ranks
+x = torch.ones(1024, device="cuda:0")
+torch.cuda.synchronize()
+rgb = np.fromfile(path, np.uint8)
+uid = gz.rccl_unique_id()
+lib = gz.rccl_library()
+coll = gz.Collectives.from_rccl(0, 0, 1, uid)
+try:
+    coll.selftest()
+    data = gz.process_strips(rgb, w, h, coll, gz.Params.for_quality(quality), device=0)
+finally:
+    coll.close()
+assert float(x.sum().item()) == 1024.0
+got = hashlib.sha256(data).hexdigest()
+print(lib)
+print(got)
+sys.exit(0 if got == want else 3)
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_beside_torch():
+    """The library's RCCL communicator in a process that imported torch and
+    initialised its device first (bench.py's ranks): the librccl is the one
+    beside the HIP runtime torch mapped (the system RCCL fails in
+    ncclCommInitRank against torch's runtime), its self-test passes and a
+    strip encode over it gives the reference's bytes (world 1,
+    GZ_STRIP_FORCE=1)."""
+    e = MANIFEST["e2e"]["bees_q95"]
+    r = subprocess.run([sys.executable, "-c", _RCCL_TORCH_CHILD,
+                        os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"), str(e["w"]), str(e["h"]),
+                        str(e["quality"]), os.path.join(GOLDEN, e["input"]), e["sha256"]],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, GZ_STRIP_FORCE="1"))
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    import torch
+    lib = r.stdout.strip().splitlines()[-2]
+    assert os.path.dirname(lib) == os.path.join(os.path.dirname(torch.__file__), "lib"), lib
+
+
 @pytest.mark.gpu
 def test_rccl_collectives_reproduce_reference():
     """The library's own RCCL communicator (gz_rccl_create: host/
@@ -265,9 +311,8 @@ def test_rccl_collectives_reproduce_reference():
     device; GZ_STRIP_FORCE=1: the strip machinery, not the single-engine
     search a one-rank split runs); the multi-GPU wiring is the same calls with
     more ranks.  In a
-    process of its own without torch, as the C++ callers it serves run: the
-    system RCCL does not initialise beside the ROCm runtime torch bundles
-    (hipGetDeviceCount fails in ncclCommInitRank once torch's is loaded)."""
+    process of its own without torch, as the C++ callers it serves run (the
+    communicator beside torch: test_rccl_collectives_beside_torch)."""
     e = MANIFEST["e2e"]["bees_q95"]
     r = subprocess.run([sys.executable, "-c", _RCCL_CHILD, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"),
                         str(e["w"]), str(e["h"]), str(e["quality"]), os.path.join(GOLDEN, e["input"]),
