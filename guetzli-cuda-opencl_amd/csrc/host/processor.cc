@@ -1909,6 +1909,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // order, for std::sort's exact permutation) only where the keys leave
       // the order open
       auto fetch_exact = [&]() -> bool {
+        const auto tf = Clock::now();
         if (!cmp_->DeviceOrderEntries(&global_order)) return false;
         if (global_order.size() != frame_n) {
           internal_err_ = "device order: entry count mismatch";
@@ -1916,16 +1917,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         }
         sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
         res_->detail["backend_order_fetches"] += 1;
+        res_->detail["backend_order_fetch_s"] += Since(tf);
         return true;
       };
       // strip_fast: this rank's entries, global_order, become the frame's (the
       // exact path) when their keys leave std::sort's order open
       auto go_exact = [&]() -> bool {
+        const auto tg = Clock::now();
         int btc = blocks_to_change;
         if (!GatherEntries(&global_order, own_lo, own_hi, gbase, &btc)) return false;
         sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
         strip_exact = true;
         res_->detail["strip_order_fallbacks"] += 1;
+        res_->detail["strip_order_fallback_s"] += Since(tg);
         return true;
       };
       const auto tc = Clock::now();
@@ -2299,8 +2303,10 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
               // the window ran out without a tie: the next one from rank s
               Engine::OrderSelection next;
               const size_t want = std::min<size_t>(8192, std::max<size_t>(512, 2 * win.size()));
+              const auto tw = Clock::now();
               if (!cmp_->DeviceSelectWindow(s, want, direction, &next)) return false;
               res_->detail["backend_tail_windows"] += 1;
+              res_->detail["backend_tail_window_s"] += Since(tw);
               if (!next.open && !next.window_overflow) {
                 win.swap(next.window);
                 win_base = s;
@@ -2310,7 +2316,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
               }
             }
             if (!fetch_exact()) return false;
+            const auto tp = Clock::now();
             if (bulk) sorter->SetPrefix(bulk);
+            res_->detail["backend_setprefix_s"] += Since(tp);
             tail_exact = true;
             res_->detail["backend_tail_exact"] += 1;
             if (!bulk && win.empty()) res_->detail["backend_tail_exact_nobulk"] += 1;
@@ -2523,12 +2531,16 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             std::vector<int> blocks;
             std::vector<float> keys;
             bool open = false;
+            const auto tn = Clock::now();
             const int r = strip_order.Next(part_, &blocks, &keys, &open);
+            res_->detail["strip_next_s"] += Since(tn);
             if (r < 0) return exchange_failed();
             if (r == 0) break;  // (no entries left on any rank)
             size_t done = 0;
             const size_t W = std::min(blocks.size(), n_order - i);
+            const auto tw = Clock::now();
             if (W && !tail_window(blocks.data(), keys.data(), W, i, &stop, &done)) return exchange_failed();
+            res_->detail["strip_window_s"] += Since(tw);
             strip_order.Consumed(done);
             i += done;
             if (!stop && open) {
@@ -2554,7 +2566,9 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
             keys[j] = global_order[i + j].second;
           }
           size_t done = 0;
+          const auto tw = Clock::now();
           if (!tail_window(blocks.data(), keys.data(), W, i, &stop, &done)) return exchange_failed();
+          res_->detail["strip_exact_window_s"] += Since(tw);
           i += done;
           window *= 2;
         }

@@ -1352,10 +1352,11 @@ struct OrdLayout {
 };
 // mapped pinned h_ord_: last_indexes [nb] bytes | totals [8] | below_floor | SelHost
 constexpr int kOrdInfoInts = 8;
-// | per k_order_build workgroup 3 ints
+// | per k_order_build workgroup 4 ints (entries, blocks with entries, below
+// the floor, the group's first entry)
 size_t OrdHostBytes(int nb) {
   return static_cast<size_t>(nb) * 4 + 64 + (sizeof(SelHost) + 63) / 64 * 64 + 64 +
-         12 * (static_cast<size_t>(nb) / kBuildBlocks + 1);
+         16 * (static_cast<size_t>(nb) / kBuildBlocks + 1);
 }
 }  // namespace
 
@@ -1484,7 +1485,7 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   ProfFlush();
   long long tot[3] = {0, 0, 0};
   for (unsigned k = 0; k < groups; ++k)
-    for (int x = 0; x < 3; ++x) tot[x] += wg[3 * k + x];
+    for (int x = 0; x < 3; ++x) tot[x] += wg[4 * k + x];
   *blocks_to_change = static_cast<int>(tot[1]);
   *n_entries = static_cast<size_t>(tot[0]);
   if (below_floor) *below_floor = tot[2];
@@ -1511,17 +1512,23 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
   GZ_HIP(WaitIdle(s));
   ProfFlush();
   // the build groups entries by workgroup in arrival order (blocks in order
-  // within a group, a block's entries in k order): a stable counting sort by
-  // block restores the block order of the host's loop
+  // within a group, a block's entries in k order), each group's position
+  // from its reservation: the groups copied in workgroup order restore the
+  // block order of the host's loop (one sequential pass; round 5 sorted by
+  // block with a counting sort, 40 ms per fetch at 8192^2)
   const auto* src = static_cast<const std::pair<int, float>*>(h_ord_entries_);
-  std::vector<int> start(static_cast<size_t>(nb_) + 1, 0);
-  for (size_t i = 0; i < n; ++i) {
-    const int b = src[i].first;
-    if (b < 0 || b >= nb_) return Fail("OrderFetch: entry block", 0);
-    ++start[b + 1];
+  const int* wg = h_ord_ + nb_ + kOrdInfoInts + 16 + static_cast<int>((sizeof(SelHost) + 63) / 64 * 16);
+  const int groups = (nb_ + kBuildBlocks - 1) / kBuildBlocks;
+  size_t at = 0;
+  for (int g = 0; g < groups; ++g) {
+    const int cnt = wg[4 * g], base = wg[4 * g + 3];
+    if (cnt == 0) continue;
+    if (cnt < 0 || base < 0 || static_cast<size_t>(base) + cnt > n || at + cnt > n)
+      return Fail("OrderFetch: workgroup ranges", 0);
+    memcpy(out + at, src + base, static_cast<size_t>(cnt) * sizeof(OrderEntry));
+    at += static_cast<size_t>(cnt);
   }
-  for (int b = 0; b < nb_; ++b) start[b + 1] += start[b];
-  for (size_t i = 0; i < n; ++i) out[start[src[i].first]++] = src[i];
+  if (at != n) return Fail("OrderFetch: entry count", 0);
   return true;
 }
 
