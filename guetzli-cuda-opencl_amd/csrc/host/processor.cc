@@ -620,12 +620,40 @@ bool HipButteraugliComparator::DeviceChangeOrder(int direction, double target_mu
   *n_entries = 0;
   for (int rblock = 1; rblock <= 4; ++rblock) {
     // (the entries are filled with the counts: one wait per radius)
-    if (!engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, n_entries, blocks_to_change,
-                             floor_limit, below_floor)) {
-      err_ = engine_->error();
-      return false;
+    const bool ok = engine_->OrderBuild(direction, rblock, td, zero_bmax, last_indexes, n_entries,
+                                        blocks_to_change, floor_limit, below_floor);
+    if (!ok) err_ = engine_->error();
+    if (order_x_) {
+      // a frame split over ranks: the radius is the first with entries
+      // anywhere in the frame; the counts are the frame's
+      uint32_t t[4] = {static_cast<uint32_t>(ok ? *n_entries : 0), static_cast<uint32_t>(ok ? *blocks_to_change : 0),
+                       static_cast<uint32_t>(ok && below_floor ? *below_floor : 0), 0};
+      if (!order_x_->SumU32(ok, t, 3)) {
+        if (ok) err_ = "change order: a rank failed";
+        return false;
+      }
+      *n_entries = t[0];
+      *blocks_to_change = static_cast<int>(t[1]);
+      if (below_floor) *below_floor = t[2];
+      engine_->SetOrderFrameEntries(*n_entries);
     }
+    if (!ok) return false;
     if (*n_entries) break;
+  }
+  return true;
+}
+
+void HipButteraugliComparator::SetDeviceOrderScope(int own_lo, int own_hi, int gbase, Engine::OrderExchange* x) {
+  order_x_ = x;
+  order_gbase_ = x ? gbase : 0;
+  if (x) engine_->SetOrderScope(own_lo, own_hi, gbase, x);
+  else engine_->SetOrderScope(0, 1 << 30, 0, nullptr);
+}
+
+bool HipButteraugliComparator::DeviceSetBlockMax(const std::vector<float>& bmax) {
+  if (static_cast<int>(bmax.size()) != engine_->blocks() || !engine_->SetBlockMax(bmax.data())) {
+    err_ = bmax.size() != static_cast<size_t>(engine_->blocks()) ? "DeviceSetBlockMax: size" : engine_->error();
+    return false;
   }
   return true;
 }
@@ -637,6 +665,9 @@ bool HipButteraugliComparator::DeviceOrderEntries(std::vector<std::pair<int, flo
     err_ = engine_->error();
     return false;
   }
+  // (a strip's entries in frame block indices, as the host build's)
+  if (order_gbase_)
+    for (auto& e : *order) e.first += order_gbase_;
   seconds_bulk += Since(t0);
   return true;
 }
@@ -646,10 +677,22 @@ bool HipButteraugliComparator::DeviceSelectBulk(const CoeffImage& img, size_t bu
   const auto t0 = Clock::now();
   if (bulk && !SyncCoeffs(img)) return false;
   int32_t delta[3][256];
-  if (!engine_->OrderSelect(bulk, window, direction, img.quant, true, sel, delta)) {
-    err_ = engine_->error();
-    return false;
+  const bool ok = engine_->OrderSelect(bulk, window, direction, img.quant, true, sel, delta);
+  if (!ok) err_ = engine_->error();
+  if (order_x_ && (!ok || sel->applied)) {
+    // a frame split over ranks: the frame's histogram change (every rank's
+    // applies to its owned blocks; the same `applied` on every rank)
+    std::vector<uint32_t> d(3 * 256);
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < 256; ++i) d[c * 256 + i] = ok ? static_cast<uint32_t>(delta[c][i]) : 0u;
+    if (!order_x_->SumU32(ok, d.data(), 3 * 256)) {
+      if (ok) err_ = "bulk prefix: a rank failed";
+      return false;
+    }
+    for (int c = 0; c < 3; ++c)
+      for (int i = 0; i < 256; ++i) delta[c][i] = static_cast<int32_t>(d[c * 256 + i]);
   }
+  if (!ok) return false;
   if (sel->applied) {
     // (the counts are stored doubled, JpegHistogram::Add)
     for (int c = 0; c < 3; ++c)
@@ -1817,8 +1860,14 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
   // the frame's candidates and block maxima are resident) unless the frame
   // is split over ranks or the comparator has no device
   bool device_order = false;
-  if ((!part_ || part_->world == 1) && cmp_->HasDeviceBulk() && !cmp_->DeviceOrderReset(&device_order))
-    return Fail(err);
+  if (cmp_->HasDeviceBulk() && !cmp_->DeviceOrderReset(&device_order)) return Fail(err);
+  // A frame split over ranks with the device order (round 6): every rank's
+  // engine builds its owned blocks' entries; the selections exchange their
+  // counts and candidates (the comparator's scope, Engine::OrderSelect), so
+  // the bulk prefix, the windows and their certification are the frame's on
+  // every rank; the owners apply the changes (their device bulk, the tail's
+  // windows through tail_window below).
+  const bool strip_dev = device_order && part_ && part_->world > 1;
   // With the device order the bulk prefix is selected and applied on the
   // device too (DeviceSelectBulk), with the change of the AC histograms
   // counted there.
@@ -1875,8 +1924,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       // entries (StripOrder below) and the frame's std::sort order is
       // derived from them where the consumed entries' keys decide it alone;
       // strip_exact: the whole frame's entries on every rank (the fallback).
-      bool strip_exact = part_ && part_->world > 1 && !StripFastOrder();
-      const bool strip_fast = part_ && part_->world > 1 && !strip_exact;
+      bool strip_exact = part_ && part_->world > 1 && !strip_dev && !StripFastOrder();
+      const bool strip_fast = part_ && part_->world > 1 && !strip_dev && !strip_exact;
       size_t frame_n = 0;
       int64_t device_below_floor = -1;
       if (device_order) {
@@ -1925,6 +1974,8 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       auto go_exact = [&]() -> bool {
         const auto tg = Clock::now();
         int btc = blocks_to_change;
+        // (the device order: this rank's entries come from its engine first)
+        if (strip_dev && !cmp_->DeviceOrderEntries(&global_order)) return false;
         if (!GatherEntries(&global_order, own_lo, own_hi, gbase, &btc)) return false;
         sorter.reset(new LazyStdSort(global_order.data(), global_order.size()));
         strip_exact = true;
@@ -1984,11 +2035,19 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         JpegHistogram ac_now[3];
         for (int c = 0; c < ncomp && c < 3; ++c) ac_now[c] = ac_histograms[c];
         if (!cmp_->DeviceSelectBulk(*img, bulk, kTailWindow, direction, &sel, ac_now)) return Fail(err);
+        // (a strip: the blocks within the halo band of its edges, which the
+        // neighbours' halos need, brought up to date and journalled at once)
+        auto strip_band = [&]() {
+          const int band = (kStripHalo / 8) * block_width;
+          for (int bix = own_lo; bix < std::min(own_hi, own_lo + band); ++bix) materialize(bix, true);
+          for (int bix = std::max(own_lo + band, own_hi - band); bix < own_hi; ++bix) materialize(bix, true);
+        };
         if (bulk && sel.applied) {
           for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
           // (the counts include the tie block's share of the K*-keyed entries)
           for (int bix = 0; bix < num_blocks; ++bix) last_indexes[bix] += sel.cnt[bix] * direction;
           img->host_partial = true;
+          if (strip_dev) strip_band();
           refresh_raw();
           loop.changed = static_cast<int>(bulk);
           res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
@@ -1998,6 +2057,37 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           // tie order decides which of them the prefix takes -- the exact
           // path (every entry, LazyStdSort), applied with the host's counts
           res_->detail["backend_select_open"] += 1;
+          if (strip_dev) {
+            // the frame's entries on every rank, the owned blocks' prefix
+            // share applied on each rank's device, the histogram change summed
+            if (!go_exact()) return exchange_failed();
+            sorter->SetPrefix(bulk);
+            bulk_cnt8.assign(num_blocks, 0);
+            for (size_t i = 0; i < bulk; ++i) {
+              const int b = global_order[i].first - gbase;
+              if (b >= own_lo && b < own_hi) ++bulk_cnt8[b];
+            }
+            int32_t delta[3][256] = {};
+            const bool ok = cmp_->DeviceBulkApplyLocal(*img, direction, bulk_cnt8.data(), last_indexes, delta);
+            std::vector<int64_t> hsum(3 * (JpegHistogram::kSize - 1) + 1, 0);
+            for (int c = 0; c < ncomp && c < 3; ++c)
+              for (int q = 0; q + 1 < JpegHistogram::kSize; ++q) hsum[c * (JpegHistogram::kSize - 1) + q] = delta[c][q];
+            hsum.back() = ok ? 0 : 1;
+            if (!part_->SumAll(hsum.data(), static_cast<int>(hsum.size()))) return exchange_failed();
+            if (!ok) return Fail(err);
+            if (hsum.back()) {
+              if (err) *err = "a rank's device bulk prefix failed";
+              return false;
+            }
+            for (int bix = own_lo; bix < own_hi; ++bix) last_indexes[bix] += bulk_cnt8[bix] * direction;
+            // (the counts are stored doubled, JpegHistogram::Add)
+            for (int c = 0; c < ncomp && c < 3; ++c)
+              for (int q = 0; q + 1 < JpegHistogram::kSize; ++q)
+                ac_histograms[c].counts[q] += 2u * static_cast<uint32_t>(hsum[c * (JpegHistogram::kSize - 1) + q]);
+            img->host_partial = true;
+            strip_band();
+            refresh_raw();
+          } else {
           if (!fetch_exact()) return Fail(err);
           sorter->SetPrefix(bulk);
           bulk_cnt8.assign(num_blocks, 0);
@@ -2008,6 +2098,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           for (int c = 0; c < ncomp && c < 3; ++c) ac_histograms[c] = ac_now[c];
           img->host_partial = true;
           refresh_raw();
+          }
           loop.changed = static_cast<int>(bulk);
           res_->detail["backend_bulk_changes"] += static_cast<double>(bulk);
           res_->detail["backend_bulk_device"] += 1;
@@ -2522,6 +2613,51 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
         };
         size_t i = bulk;
         bool stop = false;
+        if (strip_dev && !strip_exact) {
+          // the device's windows of the frame's order (certified positions);
+          // a window run out without a tie asks for the next, a tie or an
+          // overflow switches to the exact order (every rank's entries)
+          std::vector<int> blocks;
+          std::vector<float> keys;
+          while (!stop && i < n_order) {
+            if (i >= win_base + win_ok) {
+              bool got = false;
+              if (!win.empty() && win_ok == win.size() && !win_last && i == win_base + win_ok) {
+                Engine::OrderSelection next;
+                const size_t want = std::min<size_t>(8192, std::max<size_t>(512, 2 * win.size()));
+                const auto tw = Clock::now();
+                if (!cmp_->DeviceSelectWindow(i, want, direction, &next)) return Fail(err);
+                res_->detail["backend_tail_windows"] += 1;
+                res_->detail["backend_tail_window_s"] += Since(tw);
+                if (!next.open && !next.window_overflow) {
+                  win.swap(next.window);
+                  win_base = i;
+                  win_ok = next.window_ok;
+                  win_last = next.window_last;
+                  got = i < win_base + win_ok;
+                }
+              }
+              if (!got) {
+                if (!go_exact()) return exchange_failed();
+                if (bulk) sorter->SetPrefix(bulk);
+                res_->detail["backend_tail_exact"] += 1;
+                break;
+              }
+            }
+            const size_t W = std::min(win_base + win_ok, n_order) - i;
+            blocks.resize(W);
+            keys.resize(W);
+            for (size_t j = 0; j < W; ++j) {
+              blocks[j] = win[i - win_base + j].first;
+              keys[j] = win[i - win_base + j].second;
+            }
+            size_t done = 0;
+            const auto tw = Clock::now();
+            if (!tail_window(blocks.data(), keys.data(), W, i, &stop, &done)) return exchange_failed();
+            res_->detail["strip_window_s"] += Since(tw);
+            i += done;
+          }
+        }
         if (strip_fast && !strip_exact) {
           // windows of the frame's order merged from every rank's next
           // entries (StripOrder::Next); positions whose entry the keys leave
@@ -2552,7 +2688,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
           res_->detail["strip_order_fast_iters"] += strip_exact ? 0 : 1;
         }
         size_t window = 4096;
-        while ((!strip_fast || strip_exact) && !stop && i < n_order) {
+        while ((strip_dev ? strip_exact : (!strip_fast || strip_exact)) && !stop && i < n_order) {
           const size_t W = std::min(window, n_order - i);
           if (i + W > sorter->sorted()) {
             const auto ts = Clock::now();

@@ -138,6 +138,16 @@ class Comparator {
     return false;
   }
   virtual bool DeviceOrderAdvance(float val_threshold, int direction) { return false; }
+  // A frame split over ranks (host/strips.h): the device change order over
+  // this rank's owned blocks [own_lo, own_hi) of its strip, its selection
+  // over the frame through the ranks' exchange (Engine::SetOrderScope).
+  // DeviceChangeOrder's counts are then the frame's, DeviceSelectBulk's
+  // histograms the frame's change, the windows and DeviceOrderEntries in
+  // frame block indices (the entries: the owned blocks').
+  virtual void SetDeviceOrderScope(int own_lo, int own_hi, int gbase, Engine::OrderExchange* x) {}
+  // The block maxima the device change order reads: the frame's values for
+  // the strip's blocks (its own Compare's differ in the halo).
+  virtual bool DeviceSetBlockMax(const std::vector<float>& bmax) { return false; }
   // DeviceEncodeAndCompare of a candidate whose symbol histograms the caller
   // already has (the search back end tracks them exactly): the DC / AC
   // histograms SaveToJpegData + WriteJpeg would count (comps at or above
@@ -280,6 +290,8 @@ class HipButteraugliComparator : public Comparator {
                         Engine::OrderSelection* sel, JpegHistogram ac[3]) override;
   bool DeviceSelectWindow(size_t from, size_t window, int direction, Engine::OrderSelection* sel) override;
   bool DeviceOrderAdvance(float val_threshold, int direction) override;
+  void SetDeviceOrderScope(int own_lo, int own_hi, int gbase, Engine::OrderExchange* x) override;
+  bool DeviceSetBlockMax(const std::vector<float>& bmax) override;
   bool HasDeviceBulk() const override { return true; }
   bool HasKnownHistogramEncode() const override { return true; }
   bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
@@ -339,6 +351,8 @@ class HipButteraugliComparator : public Comparator {
   float distance_ = 0.0f;
   mutable std::vector<float> block_max_;
   mutable bool block_max_failed_ = false;
+  Engine::OrderExchange* order_x_ = nullptr;  // a frame split over ranks (SetDeviceOrderScope)
+  int order_gbase_ = 0;
   mutable bool block_max_stale_ = false;  // the last Compare's maxima are on the device only
   CoeffCursor device_;  // what the device copy of the coefficients reflects
   bool IsOriginal(const CoeffImage& img) const;

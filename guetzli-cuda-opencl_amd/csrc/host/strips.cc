@@ -505,6 +505,58 @@ bool PartitionComparator::Agree(bool ok, const std::string& local_err) {
   return true;
 }
 
+bool StripDeviceOrder() {
+  static const bool host = getenv("GZ_STRIP_HOST_ORDER") && atoi(getenv("GZ_STRIP_HOST_ORDER")) != 0;
+  return !host;
+}
+
+bool PartitionComparator::DeviceOrderReset(bool* available) {
+  *available = false;
+  if (part_->world == 1) return inner_->DeviceOrderReset(available) || Fail(inner_->error());
+  if (!StripDeviceOrder()) return true;
+  inner_->SetDeviceOrderScope(part_->OwnLo(), part_->OwnHi(), part_->LocalBase(), this);
+  const bool ok = inner_->DeviceOrderReset(available);
+  // agreed by every rank: a failure fails all; a rank whose buffers could
+  // not be allocated sends every rank to the host order
+  int64_t st[2] = {ok ? 0 : 1, ok && *available ? 1 : 0};
+  if (!part_->SumAll(st, 2)) return Fail("strip exchange: all-gather failed");
+  if (st[0]) return Fail(ok ? "strip exchange: a rank's device order failed" : inner_->error());
+  if (st[1] != part_->world) {
+    *available = false;
+    inner_->SetDeviceOrderScope(0, 0, 0, nullptr);
+  }
+  return true;
+}
+
+// Engine::OrderExchange: in-place sums (values as signed 32-bit: counts and
+// histogram deltas), the rank's status summed beside them
+bool PartitionComparator::SumU32(bool ok, uint32_t* v, int n) {
+  std::vector<int64_t> t(static_cast<size_t>(n) + 1);
+  for (int i = 0; i < n; ++i) t[i] = ok ? static_cast<int32_t>(v[i]) : 0;
+  t[n] = ok ? 0 : 1;
+  const auto t0 = Clock::now();
+  const bool sent = part_->SumAll(t.data(), n + 1);
+  seconds_exchange += Since(t0);
+  if (!sent || t[n]) return false;
+  for (int i = 0; i < n; ++i) v[i] = static_cast<uint32_t>(t[i]);
+  return true;
+}
+
+bool PartitionComparator::Gather(bool ok, const std::vector<unsigned long long>& mine,
+                                 std::vector<unsigned long long>* all) {
+  std::vector<uint8_t> send(mine.size() * 8);
+  if (!mine.empty()) std::memcpy(send.data(), mine.data(), send.size());
+  std::vector<std::vector<uint8_t>> got;
+  if (!Exchange(ok, "order selection", send, &got)) return false;
+  all->clear();
+  for (const auto& m : got) {
+    const size_t k = all->size();
+    all->resize(k + m.size() / 8);
+    if (!m.empty()) std::memcpy(all->data() + k, m.data(), m.size() / 8 * 8);
+  }
+  return true;
+}
+
 bool PartitionComparator::StartBlockComparisons() {
   const bool ok = inner_->StartBlockComparisons();
   return Agree(ok, ok ? "" : inner_->error());

@@ -91,7 +91,13 @@ struct Partition {
 // host).  Every call that reads the image first brings its halo rows up to
 // date with the neighbours' owned changes (a collective); the search loop
 // itself only edits owned blocks.
-class PartitionComparator : public Comparator {
+// The strips' device change order (StripDeviceOrder): every rank's engine
+// builds its owned blocks' entries, the selection exchanges its counts and
+// candidates (Engine::OrderExchange, implemented over the partition).
+// GZ_STRIP_HOST_ORDER=1: the host order (StripOrder), for A/B runs.
+bool StripDeviceOrder();
+
+class PartitionComparator : public Comparator, private Engine::OrderExchange {
  public:
   PartitionComparator(Partition* part, std::unique_ptr<Comparator> inner, float target);
   ~PartitionComparator() override;
@@ -126,14 +132,18 @@ class PartitionComparator : public Comparator {
   bool SetOriginalCoeffs(const JpegData& jpg) override;
   // One rank (the degenerate split: no halo, the strip is the frame): the
   // whole device change order and bulk prefix are the inner comparator's.
-  bool HasDeviceBulk() const override { return part_->world == 1 && inner_->HasDeviceBulk(); }
-  bool DeviceOrderReset(bool* available) override {
-    *available = false;
-    if (part_->world != 1) return true;
-    return inner_->DeviceOrderReset(available) || Fail(inner_->error());
+  // Several: the inner engine's order scoped to the owned blocks, its
+  // selection over the frame through this comparator's exchange
+  // (StripDeviceOrder; else the host order).
+  bool HasDeviceBulk() const override {
+    return (part_->world == 1 || StripDeviceOrder()) && inner_->HasDeviceBulk();
   }
+  bool DeviceOrderReset(bool* available) override;
   bool DeviceChangeOrder(int direction, double target_mul, bool zero_bmax, const std::vector<int>& last_indexes,
                          float floor_limit, size_t* n_entries, int* blocks_to_change, int64_t* below_floor) override {
+    // (the frame's maxima of the strip's blocks: its own Compare's differ
+    // in the halo, which the owned blocks' weights read up to 4 blocks deep)
+    if (part_->world != 1 && !zero_bmax && !inner_->DeviceSetBlockMax(block_max_)) return Fail(inner_->error());
     return inner_->DeviceChangeOrder(direction, target_mul, zero_bmax, last_indexes, floor_limit, n_entries,
                                      blocks_to_change, below_floor) ||
            Fail(inner_->error());
@@ -182,6 +192,9 @@ class PartitionComparator : public Comparator {
   bool Exchange(bool ok, const std::string& local_err, const std::vector<uint8_t>& send,
                 std::vector<std::vector<uint8_t>>* all);
   bool Agree(bool ok, const std::string& local_err);
+  // Engine::OrderExchange over the partition (with the status word)
+  bool SumU32(bool ok, uint32_t* v, int n) override;
+  bool Gather(bool ok, const std::vector<unsigned long long>& mine, std::vector<unsigned long long>* all) override;
   bool SyncHalo(const CoeffImage& img);
   // Codes img (headers: SaveToJpegData's, or *hdr's), overlapped with the
   // Compare of img; *size the whole file's size.

@@ -1476,6 +1476,9 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   g.wg_host = m_ord_ + nb_ + kOrdInfoInts + 16 + static_cast<int>((sizeof(SelHost) + 63) / 64 * 16);
   const int* wg = h_ord_ + nb_ + kOrdInfoInts + 16 + static_cast<int>((sizeof(SelHost) + 63) / 64 * 16);
   g.floor_limit = floor_limit;
+  g.blo = ord_lo_;
+  g.bhi = std::min(ord_hi_, nb_);
+  ord_h1_summed_ = false;
   if (direction < 0)
     GZ_TIMED("order_build", k_order_active<<<static_cast<unsigned>((nb_ + 255) / 256), 256, 0, s>>>(
                                 d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock, target_distance,
@@ -1611,7 +1614,8 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   GZ_HIP(hipSetDevice(device_));
   if (ord_cand_n_ < 0 || !d_ord_) return Fail("OrderSelect without a change order", 0);
   const size_t n = ord_n_;
-  if (n == 0 || bulk >= n || window == 0) return Fail("OrderSelect arguments", 0);
+  if ((ord_x_ ? ord_frame_n_ : n) == 0 || bulk >= (ord_x_ ? ord_frame_n_ : n) || window == 0)
+    return Fail("OrderSelect arguments", 0);
   if (!BulkCountsStaging()) return false;
   // (the candidates -- the window and the ties at its ends -- are sorted in
   // one workgroup's LDS: at most kSelCandMax; more and the host takes the
@@ -1635,8 +1639,11 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   uint8_t* cnt8 = reinterpret_cast<uint8_t*>(base + L.cnt8);
   const OrderEntry* e = static_cast<const OrderEntry*>(d_ord_entries_);
   const int has_prefix = bulk > 0 ? 1 : 0;
+  // (a frame split over ranks: ranks of the frame's order; this engine's
+  // entries are its owned blocks')
+  const size_t fn = ord_x_ ? ord_frame_n_ : n;
   const long long ta = static_cast<long long>(bulk) - 1;
-  const long long tb = static_cast<long long>(std::min(n - 1, bulk + window - 1));
+  const long long tb = static_cast<long long>(std::min(fn - 1, bulk + window - 1));
   SelHost* host = reinterpret_cast<SelHost*>(h_ord_ + nb_ + kOrdInfoInts + 16);
   SelHost* mhost = reinterpret_cast<SelHost*>(m_ord_ + nb_ + kOrdInfoInts + 16);
   host->done = 0;
@@ -1651,18 +1658,25 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   // 1080p 2050 workgroups paid that pick in 4 rounds)
   static const size_t cmax = getenv("GZ_SEL_CGROUPS") ? static_cast<size_t>(atoi(getenv("GZ_SEL_CGROUPS"))) : 512;
   const unsigned cgroups = static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(cmax, chunks)));
-  GZ_TIMED("order_select",
-           (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb,
-                                                  sel + SelLayout::h1 + ord_h1_ * kSelBins, sel,
-                                                  reinterpret_cast<uint32_t*>(cnt8), (nb_ + 3) / 4),
-            k_sel_collect<<<cgroups, kSelThreads, 0, s>>>(e, static_cast<int>(n), has_prefix,
-                                                           static_cast<long long>(bulk), ta, tb, sel,
-                                                           reinterpret_cast<uint32_t*>(cnt8),
-                                                           static_cast<unsigned long long*>(d_win_), cap),
-            k_sel_finish<<<1, kSelThreads, SelCollectLds(cap), s>>>(
-                static_cast<int>(n), has_prefix, static_cast<long long>(bulk), sel, reinterpret_cast<uint32_t*>(cnt8),
-                static_cast<const unsigned long long*>(d_win_), cap, static_cast<OrderEntry*>(m_win_), mhost,
-                force_open)));
+  uint32_t* h1 = sel + SelLayout::h1 + ord_h1_ * kSelBins;
+  const int blo = ord_x_ ? ord_lo_ : 0, bhi = ord_x_ ? std::min(ord_hi_, nb_) : nb_;
+  const int gbase = ord_x_ ? ord_gbase_ : 0;
+  if (!ord_x_) {
+    GZ_TIMED("order_select",
+             (k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb, h1, sel,
+                                                    reinterpret_cast<uint32_t*>(cnt8), (nb_ + 3) / 4),
+              k_sel_collect<<<cgroups, kSelThreads, 0, s>>>(e, static_cast<int>(n), has_prefix,
+                                                             static_cast<long long>(bulk), ta, tb, sel,
+                                                             reinterpret_cast<uint32_t*>(cnt8),
+                                                             static_cast<unsigned long long*>(d_win_), cap),
+              k_sel_finish<<<1, kSelThreads, SelCollectLds(cap), s>>>(
+                  static_cast<int>(n), has_prefix, static_cast<long long>(bulk), sel,
+                  reinterpret_cast<uint32_t*>(cnt8), static_cast<const unsigned long long*>(d_win_), cap,
+                  static_cast<OrderEntry*>(m_win_), mhost, force_open, 0, 0, nb_)));
+  } else if (!OrderSelectSplit(e, n, fn, has_prefix, bulk, ta, tb, cap, rgroups, cgroups, force_open, gbase, blo,
+                               bhi)) {
+    return false;
+  }
   if (has_prefix && apply && !BulkApplyEnqueue(direction, quant, cnt8, sel, nullptr, m_bulk_)) return false;
   GZ_HIP(WaitOnStream(s));
   ProfFlush();
@@ -1694,6 +1708,93 @@ bool Engine::OrderSelect(size_t bulk, size_t window, int direction, const int qu
   if (out->applied)
     for (int c = 0; c < 3; ++c)
       for (int i = 0; i < 256; ++i) delta[c][i] = static_cast<int32_t>(h_jhist_[(2 * c + 1) * 256 + i]);
+  return true;
+}
+
+// The selection of a frame split over ranks (SetOrderScope): the launches
+// of OrderSelect with the exchanges between them -- this build's round-1
+// counts summed once, round 2's summed, the candidates gathered from every
+// rank (frame block indices) -- then the final step alike on every rank.
+bool Engine::OrderSelectSplit(const void* entries, size_t n, size_t fn, int has_prefix, size_t bulk, long long ta,
+                              long long tb, int cap, unsigned rgroups, unsigned cgroups, int force_open, int gbase,
+                              int blo, int bhi) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  const OrderEntry* e = static_cast<const OrderEntry*>(entries);
+  const OrdLayout L(nb_);
+  char* base = static_cast<char*>(d_ord_);
+  uint32_t* sel = reinterpret_cast<uint32_t*>(base + L.sel);
+  uint32_t* cnt32 = reinterpret_cast<uint32_t*>(base + L.cnt8);
+  uint32_t* h1 = sel + SelLayout::h1 + ord_h1_ * kSelBins;
+  SelState* st = reinterpret_cast<SelState*>(sel + SelLayout::state);
+  SelHost* mhost = reinterpret_cast<SelHost*>(m_ord_ + nb_ + kOrdInfoInts + 16);
+  std::vector<uint32_t> h(2 * kSelBins);
+  // (a local failure still takes part in the exchange, with its status)
+  auto sum_counts = [&](bool ok, uint32_t* dev, int count) -> bool {
+    if (ok) ok = hipMemcpyAsync(h.data(), dev, count * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                 WaitIdle(s) == hipSuccess;
+    if (!ord_x_->SumU32(ok, h.data(), count)) return Fail("OrderSelect: exchange", 0);
+    if (!ok) return Fail("OrderSelect: counts", 0);
+    GZ_HIP(hipMemcpyAsync(dev, h.data(), count * 4, hipMemcpyHostToDevice, s));
+    return true;
+  };
+  if (!ord_h1_summed_) {
+    if (!sum_counts(true, h1, kSelBins)) return false;
+    ord_h1_summed_ = true;
+  }
+  bool ok = true;
+  GZ_TIMED("order_select", k_sel_refine<<<rgroups, 256, 0, s>>>(e, static_cast<int>(n), has_prefix, ta, tb, h1, sel,
+                                                                 cnt32, (nb_ + 3) / 4));
+  if (!sum_counts(ok, sel + SelLayout::h2, 2 * kSelBins)) return false;
+  GZ_TIMED("order_select", k_sel_collect<<<cgroups, kSelThreads, 0, s>>>(
+                               e, static_cast<int>(n), has_prefix, static_cast<long long>(bulk), ta, tb, sel, cnt32,
+                               static_cast<unsigned long long*>(d_win_), cap));
+  // this rank's candidates (their count first: more than `cap` and the
+  // merged count alone tells every rank the selection overflowed)
+  int nc = 0;
+  ok = hipMemcpyAsync(&nc, &st->cand_n, 4, hipMemcpyDeviceToHost, s) == hipSuccess && WaitIdle(s) == hipSuccess;
+  std::vector<unsigned long long> mine(1, 0ull), all;
+  if (ok && nc > 0 && nc <= cap) {
+    mine.resize(1 + static_cast<size_t>(nc));
+    ok = hipMemcpyAsync(mine.data() + 1, d_win_, static_cast<size_t>(nc) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+         WaitIdle(s) == hipSuccess;
+    for (int i = 1; i <= nc; ++i) {
+      const unsigned long long v = mine[i];
+      mine[i] = (v & 0xffffffff00000000ull) | static_cast<uint32_t>(static_cast<int>(v & 0xffffffffu) + gbase);
+    }
+  }
+  mine[0] = static_cast<unsigned long long>(std::max(nc, 0));
+  if (!ord_x_->Gather(ok, mine, &all)) return Fail("OrderSelect: candidate exchange", 0);
+  if (!ok) return Fail("OrderSelect: candidates", 0);
+  // every rank's block: [count, candidates...]
+  std::vector<unsigned long long> merged;
+  size_t total = 0;
+  for (size_t p = 0; p < all.size();) {
+    const size_t c = static_cast<size_t>(all[p]);
+    total += c;
+    const size_t have = c <= static_cast<size_t>(cap) ? c : 0;
+    if (p + 1 + have > all.size()) return Fail("OrderSelect: candidate blocks", 0);
+    merged.insert(merged.end(), all.begin() + p + 1, all.begin() + p + 1 + have);
+    p += 1 + have;
+  }
+  const int ntot = static_cast<int>(std::min<size_t>(total, 0x7fffffff));
+  if (total <= static_cast<size_t>(cap) && total)
+    GZ_HIP(hipMemcpyAsync(d_win_, merged.data(), total * 8, hipMemcpyHostToDevice, s));
+  GZ_HIP(hipMemcpyAsync(&st->cand_n, &ntot, 4, hipMemcpyHostToDevice, s));
+  GZ_TIMED("order_select", k_sel_finish<<<1, kSelThreads, SelCollectLds(cap), s>>>(
+                               static_cast<int>(fn), has_prefix, static_cast<long long>(bulk), sel, cnt32,
+                               static_cast<const unsigned long long*>(d_win_), cap,
+                               static_cast<OrderEntry*>(m_win_), mhost, force_open, gbase, blo, bhi));
+  // (the pageable sources above: the copies are done when the calls return;
+  // ntot lives until the finish launch has read it)
+  GZ_HIP(WaitIdle(s));
+  return true;
+}
+
+bool Engine::SetBlockMax(const float* bmax) {
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  GZ_HIP(hipSetDevice(device_));
+  GZ_HIP(hipMemcpyAsync(d_block_max_, bmax, static_cast<size_t>(nb_) * 4, hipMemcpyHostToDevice, s));
+  GZ_HIP(WaitIdle(s));
   return true;
 }
 

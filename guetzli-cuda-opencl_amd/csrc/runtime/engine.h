@@ -261,6 +261,34 @@ class Engine {
   bool OrderSelect(size_t bulk, size_t window, int direction, const int quant[3][64], bool apply,
                    OrderSelection* out, int32_t delta[3][256]);
 
+  // A frame split over ranks (host/strips.h): this engine's image is a
+  // strip (local blocks; frame block = gbase + local), and the change order
+  // is the frame's.  OrderBuild then forms the entries of the owned local
+  // blocks [own_lo, own_hi) only (its totals stay local: the caller sums
+  // them), and OrderSelect runs the frame-wide selection with the exchange's
+  // collectives between its launches: the round-1 and round-2 counts summed
+  // over the ranks, every rank's candidates gathered (block indices as frame
+  // indices), the final step on every rank alike -- the window in frame block
+  // indices, the prefix counts of the owned blocks.  `frame_n`: the frame's
+  // entry count (SetOrderFrameEntries after each build).  Every exchange
+  // carries a status: a rank that failed fails every rank there.
+  struct OrderExchange {
+    virtual ~OrderExchange() = default;
+    virtual bool SumU32(bool ok, uint32_t* v, int n) = 0;  // in place, over the ranks
+    virtual bool Gather(bool ok, const std::vector<unsigned long long>& mine,
+                        std::vector<unsigned long long>* all) = 0;  // every rank's, concatenated
+  };
+  void SetOrderScope(int own_lo, int own_hi, int gbase, OrderExchange* x) {
+    ord_lo_ = own_lo;
+    ord_hi_ = own_hi;
+    ord_gbase_ = gbase;
+    ord_x_ = x;
+  }
+  void SetOrderFrameEntries(size_t n) { ord_frame_n_ = n; }
+  // The block maxima the change order's weights read (the frame's values,
+  // exchanged: a strip's halo blocks differ from its own Compare's), [nb].
+  bool SetBlockMax(const float* bmax);
+
   const std::string& error() const { return err_; }
   void* stream() const { return stream_; }
   double last_kernel_ms(const char* which) const;
@@ -268,6 +296,9 @@ class Engine {
  private:
   Engine() = default;
   bool OrderEntriesCapacity(size_t n);
+  bool OrderSelectSplit(const void* entries, size_t n, size_t fn, int has_prefix, size_t bulk, long long ta,
+                        long long tb, int cap, unsigned rgroups, unsigned cgroups, int force_open, int gbase,
+                        int blo, int bhi);
   char* RequestStaging(size_t need, char** mapped);  // CompareBlocks* mapped staging
   bool AwaitPosted(const char* h, double* err);
   bool BulkCountsStaging();
@@ -382,6 +413,11 @@ class Engine {
   int* h_ord_ = nullptr;            // mapped pinned: last_indexes [nb] | totals [8]
   int* m_ord_ = nullptr;            //   (its device address)
   size_t ord_n_ = 0;                // entries of the last OrderBuild
+  // (a frame split over ranks: SetOrderScope)
+  int ord_lo_ = 0, ord_hi_ = 1 << 30, ord_gbase_ = 0;
+  OrderExchange* ord_x_ = nullptr;
+  size_t ord_frame_n_ = 0;          // the frame's entries of the last build
+  bool ord_h1_summed_ = false;      // its round-1 counts are the frame's
   void* d_ord_entries_ = nullptr;   // the entries (HBM)
   size_t d_ord_entries_cap_ = 0;
   void* h_ord_entries_ = nullptr;   // pinned: OrderFetch's staging
