@@ -460,33 +460,75 @@ bool PartitionComparator::SyncHalo(const CoeffImage& img) {
   return true;
 }
 
-bool PartitionComparator::Compare(const CoeffImage& img) {
-  if (!SyncHalo(img)) return false;
-  std::vector<float> bmax;
-  const bool ok = coder_->CompareStart(img) && coder_->Finish(&bmax, nullptr);
-  std::vector<uint8_t> send;
-  if (ok) {
-    const int lo = part_->OwnLo(), hi = part_->OwnHi();
-    send.resize((hi - lo) * sizeof(float));
-    std::memcpy(send.data(), bmax.data() + lo, send.size());
-  }
-  std::vector<std::vector<uint8_t>> all;
-  if (!Exchange(ok, coder_->err, send, &all)) return false;
-  float d = 0.0f;
+// The block rows of rank q's owned rows that another rank's back end reads:
+// the change order's block weights look kBlockMaxReach block rows past the
+// owned rows (ComputeBlockErrorAdjustmentWeights, radius <= 4: a block's
+// weight reads the activity of blocks up to 4 away, each of which reads the
+// maxima up to 4 further; butteraugli_comparator.cc:169-233), so each rank
+// sends those of its rows within that reach of another rank's owned rows.
+constexpr int kBlockMaxReach = 8;
+static std::vector<int> EdgeRows(const Partition& P, int q) {
+  std::vector<int> rows;
+  for (int y = P.row0[q]; y < P.row0[q + 1]; ++y)
+    for (int r = 0; r < P.world; ++r)
+      if (r != q && y >= P.row0[r] - kBlockMaxReach && y < P.row0[r + 1] + kBlockMaxReach) {
+        rows.push_back(y);
+        break;
+      }
+  return rows;
+}
+
+// This rank's part of a Compare's exchange: the maximum of its owned block
+// maxima (the frame's distance is the maximum of the ranks') and its edge
+// rows (EdgeRows); round 5 sent every owned block (4 MB per Compare at
+// 8192^2).  Appended to *send.
+void PartitionComparator::PackBlockMax(const std::vector<float>& bmax, std::vector<uint8_t>* send) const {
   const Partition& P = *part_;
+  float own_max = 0.0f;
+  for (int b = P.OwnLo(); b < P.OwnHi(); ++b) own_max = std::max(own_max, bmax[b]);
+  const std::vector<int> rows = EdgeRows(P, P.rank);
+  const size_t at = send->size();
+  send->resize(at + (1 + rows.size() * P.bw) * sizeof(float));
+  std::memcpy(send->data() + at, &own_max, sizeof(float));
+  for (size_t k = 0; k < rows.size(); ++k)
+    std::memcpy(send->data() + at + (1 + k * P.bw) * sizeof(float), bmax.data() + (rows[k] * P.bw - P.LocalBase()),
+                P.bw * sizeof(float));
+}
+
+// Every rank's part (all[r] from byte `skip` on) into block_max_ and the
+// distance; own: this rank's maxima.  False: a malformed part.
+bool PartitionComparator::UnpackBlockMax(const std::vector<float>& own,
+                                         const std::vector<std::vector<uint8_t>>& all, size_t skip) {
+  const Partition& P = *part_;
+  for (int b = P.OwnLo(); b < P.OwnHi(); ++b) block_max_[b] = own[b];
+  float d = 0.0f;
   for (int r = 0; r < P.world; ++r) {
-    const float* v = reinterpret_cast<const float*>(all[r].data());
-    const int n = static_cast<int>(all[r].size() / sizeof(float));
-    for (int i = 0; i < n; ++i) {
-      d = std::max(d, v[i]);
-      const int lb = P.row0[r] * P.bw + i - P.LocalBase();
-      if (lb >= 0 && lb < local_blocks_) block_max_[lb] = v[i];
+    const std::vector<int> rows = EdgeRows(P, r);
+    if (all[r].size() != skip + (1 + rows.size() * P.bw) * sizeof(float)) return false;
+    const float* v = reinterpret_cast<const float*>(all[r].data() + skip);
+    d = std::max(d, v[0]);
+    if (r == P.rank) continue;
+    for (size_t k = 0; k < rows.size(); ++k) {
+      const int lb0 = rows[k] * P.bw - P.LocalBase();
+      if (lb0 < 0 || lb0 + P.bw > local_blocks_) continue;
+      std::memcpy(block_max_.data() + lb0, v + 1 + k * P.bw, P.bw * sizeof(float));
     }
   }
   // ButteraugliScoreFromDiffmap (butteraugli.cc:1233-1240): the maximum of
   // the map is the maximum of its block maxima
   distance_ = d;
   return true;
+}
+
+bool PartitionComparator::Compare(const CoeffImage& img) {
+  if (!SyncHalo(img)) return false;
+  std::vector<float> bmax;
+  const bool ok = coder_->CompareStart(img) && coder_->Finish(&bmax, nullptr);
+  std::vector<uint8_t> send;
+  if (ok) PackBlockMax(bmax, &send);
+  std::vector<std::vector<uint8_t>> all;
+  if (!Exchange(ok, coder_->err, send, &all)) return false;
+  return UnpackBlockMax(bmax, all, 0) || Fail("strip exchange: block maxima");
 }
 
 // A local step's outcome agreed on by every rank (one small all-gather), so
@@ -734,30 +776,21 @@ bool PartitionComparator::CodeAndCompare(const CoeffImage& img, const JpegData& 
     Put(&send, part.first_word);
     Put(&send, part.last_word);
     Put(&send, static_cast<uint32_t>((part.first_shared ? 1 : 0) | (part.last_open ? 2 : 0)));
-    const size_t at = send.size();
-    send.resize(at + (m1 - m0) * sizeof(float));
-    std::memcpy(send.data() + at, bmax.data() + m0, (m1 - m0) * sizeof(float));
+    PackBlockMax(bmax, &send);
   }
   if (!Exchange(ok, coder_->err, send, &all)) return false;
   uint64_t ff = 0;
   uint32_t prev_last = 0;
-  float d = 0.0f;
   for (int r = 0; r < P.world; ++r) {
     const uint8_t* p = all[r].data();
+    if (all[r].size() < 20) return Fail("strip exchange: scan parts");
     ff += Get<uint64_t>(p);
     const uint32_t first = Get<uint32_t>(p), last = Get<uint32_t>(p), flags = Get<uint32_t>(p);
     // a word two parts share: complete once both halves are in
     if (flags & 1) ff += CountFfBytes(prev_last | first, 4);
     prev_last = last;
-    const float* v = reinterpret_cast<const float*>(p);
-    const int n = static_cast<int>((all[r].size() - 20) / sizeof(float));
-    for (int i = 0; i < n; ++i) {
-      d = std::max(d, v[i]);
-      const int lb = P.row0[r] * P.bw + i - P.LocalBase();
-      if (lb >= 0 && lb < local_blocks_) block_max_[lb] = v[i];
-    }
   }
-  distance_ = d;
+  if (!UnpackBlockMax(bmax, all, 20)) return Fail("strip exchange: block maxima");
   // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((total + 7) / 8 + ff) + 2;
   *size = cur_size_;

@@ -192,6 +192,9 @@ class PartitionComparator : public Comparator, private Engine::OrderExchange {
   bool Exchange(bool ok, const std::string& local_err, const std::vector<uint8_t>& send,
                 std::vector<std::vector<uint8_t>>* all);
   bool Agree(bool ok, const std::string& local_err);
+  // a Compare's block maxima exchange (the distance, the edge rows)
+  void PackBlockMax(const std::vector<float>& bmax, std::vector<uint8_t>* send) const;
+  bool UnpackBlockMax(const std::vector<float>& own, const std::vector<std::vector<uint8_t>>& all, size_t skip);
   // Engine::OrderExchange over the partition (with the status word)
   bool SumU32(bool ok, uint32_t* v, int n) override;
   bool Gather(bool ok, const std::vector<unsigned long long>& mine, std::vector<unsigned long long>* all) override;
