@@ -748,8 +748,8 @@ bool HipButteraugliComparator::DeviceBulkApply(const CoeffImage& img, int direct
 // symbol's low nibble).  Without the 0xff stuffing and the padding this is
 // what k_jpeg_code counts, so prologue + ceil(bits / 8) + EOI bounds the
 // candidate's size from below.
-static uint64_t ScanBits(const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
-                         const JpegCodeTables& codes) {
+uint64_t ScanBits(const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
+                  const JpegCodeTables& codes) {
   uint64_t bits = 0;
   for (int c = 0; c < ncomp; ++c)
     for (int i = 0; i < 256; ++i) {
@@ -2723,7 +2723,7 @@ bool Processor::SelectFrequencyBackEnd(const JpegData& jpg, CoeffImage* img, int
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->seconds_backend += Since(tb);
-      if (cmp_->HasKnownHistogramEncode() && !part_) {
+      if (cmp_->HasKnownHistogramEncode()) {
         // the candidate's histograms are the tracked ones: no histogram pass
         if (!EncodeAndCompareKnown(jpg, *img, saved0, dc0, ac_histograms, err)) return false;
       } else if (!EncodeAndCompare(jpg, *img, err)) {

@@ -237,6 +237,10 @@ bool PrepareScanFor(const JpegData& hdr, bool strip_metadata, int ncomp, JpegHis
 bool PrepareScan(int w, int h, const int q[3][kDCTBlockSize], const JpegData& meta,
                  bool strip_metadata, int ncomp, JpegHistogram* dc_h, JpegHistogram* ac_h,
                  std::string* prologue, JpegCodeTables* codes);
+// The scan's bit count from the histograms it is coded with (code lengths
+// plus extra bits; no stuffing, no padding): prologue + ceil(bits / 8) + EOI
+// bounds the file's size from below.
+uint64_t ScanBits(const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp, const JpegCodeTables& codes);
 
 // guetzli::ButteraugliComparator on the HIP engine.
 class HipButteraugliComparator : public Comparator {

@@ -14,6 +14,15 @@
 // with dlopen on first use (a library that never gathers does not map it).
 // tests/native/collectives_check.cc drives StagedAllGather over a
 // host-memory transport (ranks as threads) on the CPU.
+//
+// Failure behaviour: a rank whose local step fails (a staging allocation
+// or copy) returns false before it enters ncclAllGather, and its peers stay
+// blocked there -- RCCL has no timeout.  The strips' exchanges
+// (PartitionComparator::Exchange) carry a status word so that a failed
+// *search* step fails every rank in the same all-gather; a failure of the
+// transport itself leaves the job to the caller's own watchdog (as for any
+// RCCL program).  Staging buffers are allocated on the communicator's
+// device whatever device the calling thread has current.
 #pragma once
 
 #include <stddef.h>

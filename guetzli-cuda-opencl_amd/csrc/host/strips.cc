@@ -700,17 +700,56 @@ bool PartitionComparator::DeviceEncodeOriginalAndCompare(const CoeffImage& img,
   return CodeAndCompare(img, jpg_in, &hdr, strip_metadata, size);
 }
 
+bool PartitionComparator::DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta,
+                                                      bool strip_metadata, const JpegHistogram dc[3],
+                                                      const JpegHistogram ac[3], int ncomp, double best_score,
+                                                      size_t* size, bool* skipped) {
+  // The Compare first (its exchange gives every rank the frame's distance);
+  // the frame's codes from the back end's tracked histograms bound the
+  // scan's size from below (ScanBits: the exact bit count without the
+  // stuffing), so a candidate that cannot become the output (MaybeOutput,
+  // processor.cc:151-160: ScoreJPEG grows with the distance and the size)
+  // is not coded -- the same decision on every rank, from frame-wide values.
+  // A candidate that can is coded as DeviceEncodeAndCompare codes it (each
+  // rank's part offset needs its own histograms: the stage pass).
+  *skipped = false;
+  const Partition& P = *part_;
+  JpegHistogram dc_h[3], ac_h[3];
+  for (int c = 0; c < ncomp; ++c) {
+    dc_h[c] = dc[c];
+    ac_h[c] = ac[c];
+  }
+  std::string prologue;
+  JpegCodeTables codes;
+  if (!PrepareScan(P.width, P.height, img.quant, meta, strip_metadata, ncomp, dc_h, ac_h, &prologue, &codes))
+    return Fail("strip coder: jpeg header");
+  const size_t size_lb = prologue.size() + static_cast<size_t>((ScanBits(dc, ac, ncomp, codes) + 7) / 8) + 2;
+  if (!Compare(img)) return false;
+  if (best_score >= 0 && scan_bound_mismatches == 0 && ScoreJPEG(distance_, static_cast<int>(size_lb), target_) >= best_score) {
+    *skipped = true;
+    ++scans_skipped;
+    return true;
+  }
+  if (!CodeAndCompare(img, meta, nullptr, strip_metadata, size, /*compare=*/false)) return false;
+  // (the coded scan's bits are the histograms'; a mismatch would make the
+  // bound unsafe: later candidates are then always coded)
+  if (cur_size_ < size_lb) ++scan_bound_mismatches;
+  return true;
+}
+
 bool PartitionComparator::CodeAndCompare(const CoeffImage& img, const JpegData& meta,
-                                         const JpegData* hdr, bool strip_metadata, size_t* size) {
+                                         const JpegData* hdr, bool strip_metadata, size_t* size,
+                                         bool compare) {
   // one stream order per rank: histogram stage, Compare pass; the
   // histograms' exchange and the codes while the pass runs; the scan part at
-  // this rank's offset; then the maxima and the parts' seams.
+  // this rank's offset; then the maxima and the parts' seams.  (compare
+  // false: the Compare of img has been done; the scan alone.)
   if (!SyncHalo(img)) return false;
   const Partition& P = *part_;
   const int m0 = P.OwnLo(), m1 = P.OwnHi();
   uint32_t hist[6 * 256];
   uint64_t chroma = 0;
-  bool ok = coder_->StageStart(img, m0, m1) && coder_->CompareStart(img) &&
+  bool ok = coder_->StageStart(img, m0, m1) && (!compare || coder_->CompareStart(img)) &&
             coder_->StageWait(hist, &chroma);
   std::vector<uint8_t> send;
   if (ok) {
@@ -776,7 +815,7 @@ bool PartitionComparator::CodeAndCompare(const CoeffImage& img, const JpegData& 
     Put(&send, part.first_word);
     Put(&send, part.last_word);
     Put(&send, static_cast<uint32_t>((part.first_shared ? 1 : 0) | (part.last_open ? 2 : 0)));
-    PackBlockMax(bmax, &send);
+    if (compare) PackBlockMax(bmax, &send);
   }
   if (!Exchange(ok, coder_->err, send, &all)) return false;
   uint64_t ff = 0;
@@ -790,7 +829,7 @@ bool PartitionComparator::CodeAndCompare(const CoeffImage& img, const JpegData& 
     if (flags & 1) ff += CountFfBytes(prev_last | first, 4);
     prev_last = last;
   }
-  if (!UnpackBlockMax(bmax, all, 20)) return Fail("strip exchange: block maxima");
+  if (compare && !UnpackBlockMax(bmax, all, 20)) return Fail("strip exchange: block maxima");
   // prologue + scan bytes (padded) + a stuffed 0x00 per 0xff + EOI
   cur_size_ = cur_prologue_.size() + static_cast<size_t>((total + 7) / 8 + ff) + 2;
   *size = cur_size_;

@@ -113,6 +113,14 @@ class PartitionComparator : public Comparator, private Engine::OrderExchange {
   bool QuantizeFromOriginal(const int q[3][kDCTBlockSize], CoeffImage* img,
                             bool need_host = true) override;
   bool HasDeviceWriter() const override { return true; }
+  // The back end's candidates, coded from its tracked (frame) histograms:
+  // not coded at all when the bound on their size shows they cannot win.
+  bool HasKnownHistogramEncode() const override { return true; }
+  bool DeviceEncodeAndCompareKnown(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
+                                   const JpegHistogram dc[3], const JpegHistogram ac[3], int ncomp,
+                                   double best_score, size_t* size, bool* skipped) override;
+  int scan_bound_mismatches = 0;
+  int scans_skipped = 0;
   bool DeviceEncodeAndCompare(const CoeffImage& img, const JpegData& meta, bool strip_metadata,
                               size_t* size) override;
   bool DeviceEncodeOriginalAndCompare(const CoeffImage& img, const JpegData& jpg_in,
@@ -202,7 +210,7 @@ class PartitionComparator : public Comparator, private Engine::OrderExchange {
   // Codes img (headers: SaveToJpegData's, or *hdr's), overlapped with the
   // Compare of img; *size the whole file's size.
   bool CodeAndCompare(const CoeffImage& img, const JpegData& meta, const JpegData* hdr,
-                      bool strip_metadata, size_t* size);
+                      bool strip_metadata, size_t* size, bool compare = true);
 
   Partition* part_;
   std::unique_ptr<Comparator> inner_;

@@ -282,6 +282,7 @@ import numpy as np
 sys.path.insert(0, sys.argv[1])
 import guetzli_amd as gz
 spare_xcd = int(sys.argv[3])
+ncoders = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 L = ctypes.CDLL(sys.argv[2])
 L.occupy_start.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
 L.occupy_start.restype = ctypes.c_void_p
@@ -296,7 +297,7 @@ qq = quant[:, None, :]
 r = np.fmod(c, qq)
 co = (c + np.where(2 * r > qq, qq - r, np.where(-2 * r > qq, -qq - r, -r))).astype(np.int16).reshape(-1)
 host = gz.write_jpeg_host(co, quant, w, h)
-cmps = [gz.ButteraugliComparator(w, h, rgb, 1.0) for _ in range(3)]
+cmps = [gz.ButteraugliComparator(w, h, rgb, 1.0) for _ in range(ncoders)]
 warm = all(cm.write_jpeg(co, quant) == host for cm in cmps)
 occ = L.occupy_start(0, spare_xcd, 20000)
 assert occ, "occupy_start failed"
@@ -304,7 +305,7 @@ released = False
 try:
     time.sleep(0.2)
     held = L.occupy_held(occ)
-    with concurrent.futures.ThreadPoolExecutor(max_workers=3) as ex:
+    with concurrent.futures.ThreadPoolExecutor(max_workers=ncoders) as ex:
         futs = [ex.submit(cm.write_jpeg, co, quant) for cm in cmps]
         done, pending = concurrent.futures.wait(futs, timeout=12.0)
         still_held = L.occupy_held(occ)
@@ -319,8 +320,8 @@ print(json.dumps({"warm": warm, "held": held, "still_held": still_held, "pending
 """
 
 
-@pytest.mark.parametrize("spare_xcd", [0, 5])
-def test_coder_forward_progress_under_occupancy(spare_xcd):
+@pytest.mark.parametrize("spare_xcd,queues,coders", [(0, 16, 3), (5, 16, 3)])
+def test_coder_forward_progress_under_occupancy(spare_xcd, queues, coders):
     """k_jpeg_code never waits without bound on a workgroup that has not been
     dispatched (jpeg_kernels.inc: look-back fallback + seam counters).
     Another stream's kernel holds every CU but those of one XCD (one
@@ -330,14 +331,18 @@ def test_coder_forward_progress_under_occupancy(spare_xcd):
     writer's bytes.  In a process of its own with 16 hardware queues: with
     the default 4, a coder's stream may share the holding kernel's queue and
     then waits behind it in queue order (the runtime's stream-to-queue
-    assignment, not the coder) -- round 5 saw exactly that."""
+    assignment, not the coder) -- round 5 saw exactly that.  At the
+    shipped default of 4 queues the holding kernel itself could not be
+    placed on a queue of its own (round 6: with two coders it never started
+    while they ran, `held` 0), so forward progress there is argued from the
+    kernel's bounded waits, not tested."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     pkg = os.path.join(here, "..", "guetzli-cuda-opencl_amd", "python")
     lib = os.path.join(here, "_build", "libgz_occupy.so")
-    res = subprocess.run([sys.executable, "-c", _OCCUPY_RUN, pkg, lib, str(spare_xcd)],
-                         env=dict(os.environ, GPU_MAX_HW_QUEUES="16"), capture_output=True, text=True,
+    res = subprocess.run([sys.executable, "-c", _OCCUPY_RUN, pkg, lib, str(spare_xcd), str(coders)],
+                         env=dict(os.environ, GPU_MAX_HW_QUEUES=str(queues)), capture_output=True, text=True,
                          timeout=240)
     assert res.returncode == 0, res.stderr[-3000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
