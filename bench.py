@@ -146,7 +146,7 @@ BLUR_MASK_STAGES = ("opsin_mhic", "edge_mask", "blur_h", "blur_v", "combine", "d
 STAGE_SYMBOL = {
     "coeffs_to_linear": "gz::k_coeffs_to_srgb8(", "opsin_mhic": "gz::k_opsin_mhic_stream(",
     "edge_blur": "void gz::k_blur_stream<2>(", "edge_map": "gz::k_edge_map(",
-    "block_diff": "gz::k_block_diff(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
+    "block_diff": "gz::k_block_diff2(", "lowfreq_blur_h": "void gz::k_blur_h4<3,",
     "lowfreq_blur_v": "void gz::k_blur_vstream<3>(", "low_freq": "gz::k_low_freq(",
     "mask_front": "gz::k_mask_stream(", "edge_mask": "gz::k_edge_mask_stream(",
     "blur_h": "void gz::k_blur_h4<6,", "blur_v": "void gz::k_blur_vstream<6>(",

@@ -821,7 +821,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     return true;
   };
   ProfBegin("compare_pass");
-  // Res points that k_edge_map / k_block_diff skip are never read by
+  // Res points that k_edge_map / k_block_diff2 skip are never read by
   // k_combine (it reads only ry + 5 < h, rx + 5 < w, all written this pass),
   // so the zeroing is only for the stage dumps, which compare whole arrays.
   if (dbg) {
@@ -865,7 +865,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     GZ_TIMED("edge_mask", k_edge_mask_stream<<<(waves + 3) / 4, 256, 0, s>>>(
         d_m0_, d_m1_, w_, h_, strips, segs, rows, d_bl_, d_mb_, d_scales_, scale_stride_));
   }
-  // (the search's passes compute the edge term in k_block_diff; the stage
+  // (the search's passes compute the edge term in k_block_diff2; the stage
   // dumps keep k_edge_map, whose output they read before block_diff runs)
   static const bool fuse_env = !getenv("GZ_FUSE_EDGE") || atoi(getenv("GZ_FUSE_EDGE")) != 0;
   const bool prod = dbg && dbg->production;
@@ -873,17 +873,11 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
   if (!fuse_edge)
     GZ_TIMED("edge_map", k_edge_map<<<PixGrid(rw_, rh_), 256, 0, s>>>(d_bl_, d_bl_ + 3 * n, w_, h_, rw_, rh_, d_edge_));
   if (dbg && !fuse_edge && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
-  // S6: block diff (GZ_BD2=0: the one-lane-per-res-point form, for A/B runs)
-  static const bool bd2 = !getenv("GZ_BD2") || atoi(getenv("GZ_BD2")) != 0;
-  if (bd2)
-    GZ_TIMED("block_diff", k_block_diff2<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), kBd2Threads, 0, s>>>(
-        d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_, fuse_edge ? d_bl_ : nullptr,
-        fuse_edge ? d_bl_ + 3 * n : nullptr, d_edge_));
-  else
-    GZ_TIMED("block_diff", k_block_diff<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), kBdThreads, 0, s>>>(
-        d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_, fuse_edge ? d_bl_ : nullptr,
-        fuse_edge ? d_bl_ + 3 * n : nullptr, d_edge_));
-  // (the fused edge term is in d_edge_ once k_block_diff has run)
+  // S6: block diff
+  GZ_TIMED("block_diff", k_block_diff2<<<dim3((rw_ + kBdT - 1) / kBdT, (rh_ + kBdT - 1) / kBdT), kBd2Threads, 0, s>>>(
+      d_m0_, d_m1_, w_, h_, rw_, rh_, d_dc_, d_ac_, fuse_edge ? d_bl_ : nullptr,
+      fuse_edge ? d_bl_ + 3 * n : nullptr, d_edge_));
+  // (the fused edge term is in d_edge_ once k_block_diff2 has run)
   if (dbg && fuse_edge && !d2h(dbg->edge, d_edge_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_dc, d_dc_, 3 * rn)) return false;
   if (dbg && !d2h(dbg->block_ac, d_ac_, 3 * rn)) return false;

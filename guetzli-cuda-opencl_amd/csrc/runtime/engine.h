@@ -46,7 +46,7 @@ struct CompareDebug {
   float* combined = nullptr;      // rw*rh
   float* distmap = nullptr;       // w*h
   // Dump from the search's own kernel variants (the corner edge term fused
-  // into k_block_diff, the low-frequency term into k_combine_channels, the
+  // into k_block_diff2, the low-frequency term into k_combine_channels, the
   // subsampled B mask, the mask LUTs in the vertical blur's epilogue) instead
   // of switching to the stand-alone dump kernels.  Only the planes those
   // variants leave in HBM can be dumped: mhic0, mhic1, edge, block_dc,

@@ -70,7 +70,7 @@ PROD_STAGES = ["mhic0", "mhic1", "edge", "block_dc", "block_ac", "distmap"]
 
 @pytest.mark.parametrize("case", fixture_cases())
 def test_production_stages_bit_exact(gz, case):
-    """The planes of the search's own kernel variants (k_block_diff with the
+    """The planes of the search's own kernel variants (k_block_diff2 with the
     corner edge term fused in, k_combine_channels with the low-frequency term
     and the subsampled B mask, the LUT epilogue of the vertical blur) against
     the reference's stage dumps -- not the stand-alone dump kernels that

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # dominant global load width (bytes per lane) of each kernel, from the
 # gfx950 assembly (global_load_dword / _dwordx2 / _dwordx4 counts)
-READ_WIDTH = {"k_blur_vstream": 8, "k_block_diff": 8, "k_jpeg_stage": 16}
+READ_WIDTH = {"k_blur_vstream": 8, "k_block_diff2": 8, "k_block_diff": 8, "k_jpeg_stage": 16}
 
 
 def load(d, counter):
