@@ -441,6 +441,7 @@ void SubsampledPlane::Update(int bx, int by, const uint8_t idct[64]) {
 }
 
 void Image420::Init(int width, int height) {
+  SavedReset();
   w = width;
   h = height;
   bw = (w + 7) / 8;
@@ -459,6 +460,7 @@ void Image420::Init(int width, int height) {
 void Image420::SetCoeffBlock(int comp, int b, const coeff_t* blk) {
   coeff_t* dst = block(comp, b);
   if (dst != blk) std::memcpy(dst, blk, 64 * sizeof(coeff_t));
+  if (saved_ok_) dirty_[comp].push_back(b);
   if (comp == 0) return;  // factor 1: the pixels are the IDCT, formed on the device
   uint8_t idct[64];
   BlockIdctBytes(dst, idct);
@@ -466,6 +468,7 @@ void Image420::SetCoeffBlock(int comp, int b, const coeff_t* blk) {
 }
 
 void Image420::CopyFromJpegData(const JpegData& jpg) {
+  SavedReset();
   for (int comp = 0; comp < 3; ++comp) {
     const JpegComponent& jc = jpg.components[comp];
     const int* q = jpg.quant[jc.quant_idx].values;
@@ -483,6 +486,7 @@ void Image420::CopyFromJpegData(const JpegData& jpg) {
 }
 
 void Image420::ApplyGlobalQuantization(const int q[3][kDCTBlockSize]) {
+  SavedReset();
   for (int comp = 0; comp < 3; ++comp) {
     const int nb = Blocks(comp);
     for (int b = 0; b < nb; ++b) {
@@ -544,6 +548,33 @@ void Image420::SaveToJpegData(JpegData* jpg) const {
       }
   }
   SaveQuantTables(quant, jpg);
+}
+
+const JpegData& Image420::SavedJpegData(const JpegData& meta) {
+  const int ncomp = ChromaAllZero() ? 1 : 3;
+  bool whole = !saved_ok_ || static_cast<int>(saved_.components.size()) != ncomp;
+  for (int comp = 0; comp < ncomp && !whole; ++comp) {
+    JpegComponent& jc = saved_.components[comp];
+    const int nbw = BlockWidth(comp);
+    for (const int b : dirty_[comp]) {
+      const coeff_t* src = block(comp, b);
+      coeff_t* dst = &jc.coeffs[(static_cast<size_t>(b / nbw) * jc.width_in_blocks + b % nbw) * 64];
+      const coeff_t dc = static_cast<coeff_t>(src[0] / quant[comp][0]);
+      if (dc != dst[0]) {
+        whole = true;
+        break;
+      }
+      for (int k = 1; k < 64; ++k) dst[k] = static_cast<coeff_t>(src[k] / quant[comp][k]);
+    }
+  }
+  if (whole) {
+    SaveToJpegData(&saved_);
+    saved_.app_data = meta.app_data;
+    saved_.com_data = meta.com_data;
+    saved_ok_ = true;
+  }
+  for (auto& d : dirty_) d.clear();
+  return saved_;
 }
 
 bool DownsampleToJpegData420(const JpegData& jpg444, bool silver_screen, JpegData* jpg420) {

@@ -70,6 +70,22 @@ struct Image420 {
   // SaveToJpegData (output_image.cc:579-640): Y 2x2 / chroma 1x1 MCUs
   // (1 component when both chroma planes are all zero).
   void SaveToJpegData(JpegData* jpg) const;
+  // SaveToJpegData over meta's app / com data, kept current between calls:
+  // the blocks SetCoeffBlock changed since the last call re-quantized, the
+  // rest as saved (a whole SaveToJpegData after Init / CopyFromJpegData /
+  // ApplyGlobalQuantization, a changed DC -- padding blocks repeat the last
+  // DC -- or a changed component count).  The search writes one candidate
+  // per iteration and changes few blocks between them.
+  const JpegData& SavedJpegData(const JpegData& meta);
+
+  JpegData saved_;
+  bool saved_ok_ = false;
+  std::vector<int> dirty_[3];  // blocks set since the last SavedJpegData
+ private:
+  void SavedReset() {
+    saved_ok_ = false;
+    for (auto& d : dirty_) d.clear();
+  }
 };
 
 // Processor::DownsampleImage + OutputImage::Downsample + SaveToJpegData

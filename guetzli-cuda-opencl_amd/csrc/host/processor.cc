@@ -1204,15 +1204,37 @@ struct AcBlockModel {
     if (kRaw) *raw += weight * bits;
   }
 
+  // The 4:2:0 image's blocks (Y, then Cb, Cr at factor 2): slot base[c] + b.
+  void Build(const Image420& img, size_t base[3]) {
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < kDCTBlockSize; ++k) inv_q[c][k] = 1.0f / static_cast<float>(img.quant[c][k]);
+    base[0] = 0;
+    base[1] = static_cast<size_t>(img.Blocks(0));
+    base[2] = base[1] + static_cast<size_t>(img.Blocks(1));
+    nz.assign(base[2] + static_cast<size_t>(img.Blocks(2)), 0);
+    for (int c = 0; c < 3; ++c)
+      for (int b = 0; b < img.Blocks(c); ++b) {
+        const coeff_t* blk = img.block(c, b);
+        uint64_t m = 0;
+        for (int z = 0; z < 64; ++z) m |= static_cast<uint64_t>(blk[kJPEGNaturalOrder[z]] != 0) << z;
+        nz[base[c] + b] = m;
+      }
+  }
+
   // block[k] := newval with the histogram / raw-bit bookkeeping.
   template <class H, bool kRaw = true>
   void Change(int c, int bix, int blocks, coeff_t* block, int k, coeff_t newval, const int* q,
               const uint8_t* depth, H* h, int64_t* raw) {
+    ChangeAt<H, kRaw>(static_cast<size_t>(c) * blocks + bix, c, block, k, newval, q, depth, h, raw);
+  }
+  template <class H, bool kRaw = true>
+  void ChangeAt(size_t slot, int c, coeff_t* block, int k, coeff_t newval, const int* q, const uint8_t* depth,
+                H* h, int64_t* raw) {
     const coeff_t old = block[k];
     block[k] = newval;
     const int z = kJPEGZigZagOrder[k];
     if (z == 0 || old == newval) return;  // DC is not an AC symbol
-    uint64_t& m = nz[static_cast<size_t>(c) * blocks + bix];
+    uint64_t& m = nz[slot];
     const uint64_t below = m & ((1ull << z) - 1) & ~1ull;
     const uint64_t above = z < 63 ? m & ~((2ull << z) - 1) : 0;
     const int p = below ? 63 - __builtin_clzll(below) : 0;
@@ -1708,6 +1730,7 @@ class Processor {
                          Image420* img, QuantData* data, std::string* err);
   bool SelectFrequencyMasking420(const JpegData& jpg, Image420* img, int comp_mask,
                                  double target_mul, bool stop_early, std::string* err);
+  void BeginOutput420(const JpegData& jpg, Image420* img);
 
   ProcessParams params_;
   Comparator* cmp_;
@@ -3169,20 +3192,53 @@ bool Processor::TryQuantMatrix420(const JpegData& jpg, float target_mul, const i
   img->CopyFromJpegData(jpg);
   img->ApplyGlobalQuantization(q);
   res_->seconds_quantize += Since(tq);
+  FlushOutput();
+  // the candidate's bytes on a helper thread while its Compare runs (the
+  // size is needed at once: joined before the return)
+  const auto te = Clock::now();
+  const JpegData& out = img->SavedJpegData(jpg);
+  res_->detail["r420_stage_s"] += Since(te);
   std::string encoded;
-  {
-    JpegData out;
-    out.app_data = jpg.app_data;
-    out.com_data = jpg.com_data;
-    img->SaveToJpegData(&out);
-    OutputJpeg(out, &encoded);
-  }
+  double enc_s = 0.0;
+  std::thread wr([&] {
+    const auto t = Clock::now();
+    WriteJpeg(out, params_.clear_metadata, &encoded);
+    enc_s = Since(t);
+  });
   ++res_->iterations;
-  if (!cmp_->Compare420(*img)) return Fail(err);
+  const auto tc = Clock::now();
+  const bool ok = cmp_->Compare420(*img);
+  res_->detail["r420_compare_s"] += Since(tc);
+  const auto tw = Clock::now();
+  wr.join();
+  res_->detail["write_wait_s"] += Since(tw);
+  res_->seconds_write += enc_s;
+  res_->detail["write_jpeg_s"] += enc_s;
+  if (!ok) return Fail(err);
   data->dist_ok = cmp_->DistanceOK(target_mul);
   data->jpg_size = encoded.size();
   MaybeOutput(encoded);
   return true;
+}
+
+// A 4:2:0 back-end candidate's output (processor.cc:899-904 after the
+// iteration's changes): its bytes formed on the helper thread while the
+// Compare that scores it and the next iteration's selection run;
+// FlushOutput applies its MaybeOutput before the next Compare.
+void Processor::BeginOutput420(const JpegData& jpg, Image420* img) {
+  FlushOutput();
+  const auto te = Clock::now();
+  const JpegData& out = img->SavedJpegData(jpg);
+  res_->detail["r420_stage_s"] += Since(te);
+  pending_.clear();
+  pending_device_ = false;
+  pending_skipped_ = false;
+  writer_ = std::thread([this, &out] {
+    const auto t = Clock::now();
+    WriteJpeg(out, params_.clear_metadata, &pending_);
+    encode_s_ = Since(t);
+  });
+  has_pending_ = true;
 }
 
 bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, int comp_mask,
@@ -3198,6 +3254,8 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
   const int block_width = (w + 8 * factor - 1) / (8 * factor);
   const int block_height = (h + 8 * factor - 1) / (8 * factor);
   const int num_blocks = block_width * block_height;
+  FlushOutput();  // (the last candidate's MaybeOutput sees its own Compare's distance)
+  const auto tz = Clock::now();
   if (!cmp_->StartBlockComparisons()) return Fail(err);
   std::vector<int> offsets;
   std::vector<uint8_t> cand;
@@ -3206,6 +3264,7 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
                                        params_.new_zeroing_model, &offsets, &cand, &cand_err))
     return Fail(err);
   cmp_->FinishBlockComparisons();
+  res_->detail[comp_mask == 1 ? "r420_zeroing_y_s" : "r420_zeroing_c_s"] += Since(tz);
   res_->detail["candidates"] += static_cast<double>(cand.size());
   const auto tb0 = Clock::now();
   std::vector<JpegHistogram> ac_histograms(ncomp);
@@ -3232,6 +3291,12 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
   int prev_size = base_size;
   std::vector<float> max_block_error(num_blocks, 0.0f);
   std::vector<int> last_indexes(num_blocks, 0);
+  // (a change's symbol updates from its neighbours in zigzag order, as the
+  // 4:4:4 back end; UpdateACHistogram's two passes over the block give the
+  // same counts)
+  AcBlockModel acm;
+  size_t acm_base[3];
+  acm.Build(*img, acm_base);
   res_->seconds_backend += Since(tb0);
   bool first_up_iter = true;
   for (int direction : {1, -1}) {
@@ -3261,6 +3326,7 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
                             last_indexes, offsets, cand_err, max_block_error, &global_order,
                             &block_weight, &blocks_to_change))
         return Fail(err);
+      res_->detail["r420_order_s"] += Since(tb);
       if (global_order.empty()) {
         res_->seconds_backend += Since(tb);
         break;
@@ -3285,12 +3351,10 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
         const int jpg_bix = by * comp.width_in_blocks + bx;
         const int newval =
             direction > 0 ? 0 : QuantizeCoeff(comp.coeffs[static_cast<size_t>(jpg_bix) * 64 + k], quant[k]);
-        coeff_t block[kDCTBlockSize];
-        std::memcpy(block, img->block(c, bix), sizeof(block));
-        UpdateACHistogram(-1, block, quant, &ac_histograms[c]);
-        block[k] = static_cast<coeff_t>(newval);
-        UpdateACHistogram(1, block, quant, &ac_histograms[c]);
-        img->SetCoeffBlock(c, bix, block);
+        coeff_t* block = img->block(c, bix);
+        acm.ChangeAt<JpegHistogram, false>(acm_base[c] + bix, c, block, k, static_cast<coeff_t>(newval), quant,
+                                           nullptr, &ac_histograms[c], nullptr);
+        img->SetCoeffBlock(c, bix, block);  // (the chroma's pixel update)
         last_indexes[bix] += direction;
         loop.Applied(global_order[i].second);
         if (loop.CodesRead(i)) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
@@ -3304,16 +3368,10 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->detail["backend420_changes"] += loop.changed;
       res_->seconds_backend += Since(tb);
-      std::string encoded;
-      {
-        JpegData out;
-        out.app_data = jpg.app_data;
-        out.com_data = jpg.com_data;
-        img->SaveToJpegData(&out);
-        OutputJpeg(out, &encoded);
-      }
+      BeginOutput420(jpg, img);
+      const auto tc = Clock::now();
       if (!cmp_->Compare420(*img)) return Fail(err);
-      MaybeOutput(encoded);
+      res_->detail["r420_compare_s"] += Since(tc);
       prev_size = est_jpg_size;
     }
   }

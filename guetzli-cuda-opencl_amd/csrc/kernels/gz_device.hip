@@ -1860,7 +1860,7 @@ bool Engine::BlockZeroingCandidates420(int comp_mask, float limit, int lookahead
   for (int t = 0; t <= (cbw_ - 1) + 2 * (cbh_ - 1); ++t) {
     const int lo = std::max(0, (t - (cbw_ - 1) + 1) / 2), hi = std::min(cbh_ - 1, t / 2);
     if (lo > hi) continue;
-    k_block_zeroing420<<<hi - lo + 1, 64, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
+    k_block_zeroing420<<<hi - lo + 1, kZ4Threads, 0, s>>>(d_cur_, d_orig_, d_rgb_, d_mask_scale_, w_, h_, bw_, nb_,
                                                   cbw_, t, lo, limit, lookahead, new_model ? 1 : 0, d_planes_,
                                                   static_cast<CoeffData*>(d_zero_out_), d_zero_count_);
     GZ_HIP(hipGetLastError());

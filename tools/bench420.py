@@ -26,6 +26,7 @@ def main():
         t0 = time.perf_counter()
         data, st = gz.process(rgb, w, h, p, return_stats=True)
         dt = time.perf_counter() - t0
+        detail = gz.last_process_detail()
         # a second run with per-launch timing (no graphs: slower, for the split)
         gz.profile_enable(True)
         gz.profile_reset()
@@ -41,7 +42,7 @@ def main():
                           "seconds_write": round(st.seconds_write, 4),
                           "seconds_backend": round(st.seconds_backend, 4),
                           "seconds_quantize": round(st.seconds_quantize, 4),
-                          "kernel_ms_total": kern}), flush=True)
+                          "kernel_ms_total": kern, "detail": detail}), flush=True)
 
 
 if __name__ == "__main__":
