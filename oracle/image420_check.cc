@@ -144,16 +144,30 @@ int main(int argc, char** argv) {
   rimg.ApplyGlobalQuantization(q);
   oimg.ApplyGlobalQuantization(q);
   if (!SamePlanes(rimg, oimg, "ApplyGlobalQuantization")) return 1;
+  // (with Y edits too, and Image420::SavedJpegData -- the search's
+  // incrementally kept SaveToJpegData -- checked against the reference's
+  // whole SaveToJpegData eight times along the way)
   const int nb = oimg.cbw * oimg.cbh;
-  for (int step = 0; step < 4 * nb; ++step) {
-    const int c = 1 + static_cast<int>(Next() % 2);
-    const int b = static_cast<int>(Next() % nb);
+  const int steps = 4 * nb;
+  oimg.SavedJpegData(ojpg);
+  for (int step = 0; step < steps; ++step) {
+    const int c = static_cast<int>(Next() % 3);
+    const int nbc = c == 0 ? oimg.bw * oimg.bh : nb, bwc = c == 0 ? oimg.bw : oimg.cbw;
+    const int b = static_cast<int>(Next() % nbc);
     gz::coeff_t blk[64];
     std::memcpy(blk, oimg.block(c, b), sizeof(blk));
     const int k = static_cast<int>(Next() % 64);
     blk[k] = static_cast<gz::coeff_t>(Next() % 3 == 0 ? 0 : blk[k] + q[c][k] * (static_cast<int>(Next() % 5) - 2));
-    rimg.component(c).SetCoeffBlock(b % oimg.cbw, b / oimg.cbw, blk);
+    rimg.component(c).SetCoeffBlock(b % bwc, b / bwc, blk);
     oimg.SetCoeffBlock(c, b, blk);
+    if ((step + 1) % ((steps + 7) / 8) == 0 || step + 1 == steps) {
+      guetzli::JPEGData rj = rjpg;
+      rimg.SaveToJpegData(&rj);
+      if (!SameJpegData(rj, oimg.SavedJpegData(ojpg))) {
+        fprintf(stderr, "SavedJpegData after %d edits\n", step + 1);
+        return 1;
+      }
+    }
   }
   if (!SamePlanes(rimg, oimg, "SetCoeffBlock sequence")) return 1;
 
