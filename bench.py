@@ -782,7 +782,15 @@ def main():
         host[k] = getattr(st1, k)
     host.update(gz.last_process_detail())
 
-    large = None if args.no_large_frame else large_frame(gz, dist, world, rank, dev)
+    large = None
+    if not args.no_large_frame:
+        # (a side leg after the timed region: a failure there is reported in
+        # the line instead of losing it)
+        try:
+            large = large_frame(gz, dist, world, rank, dev)
+        except Exception as e:  # noqa: BLE001
+            large = {"config": "BASELINE configs[4]", "error": repr(e)[:400]}
+            print("configs[4] leg failed on rank %d: %r" % (rank, e), file=sys.stderr, flush=True)
     if rank != 0:
         pool.shutdown()
         if dist is not None:
