@@ -181,6 +181,17 @@ def main():
             cases.append(("%s_q%d_%s%s" % (name, q, "try420" if "try_420" in params else "force420",
                                            "_" + tag if tag else ""), rgb, w, h, q, params))
         run_e2e(manifest, cases, section="e2e_420")
+    if "e2e-420-la" in what:
+        # lookahead other than 3 in the 4:2:0 chroma search (k_block_zeroing420
+        # evaluates a step's candidates three at a time: 2 is one short group,
+        # 4 and 5 a full group and a short one)
+        cases = []
+        for name, q, la in [("tex_64x48", 95, 2), ("tex_64x48", 95, 4), ("tex_100x77", 95, 5)]:
+            d = os.path.join(HERE, "stages_" + name)
+            meta = dict(l.split() for l in open(os.path.join(d, "meta.txt")) if len(l.split()) == 2)
+            cases.append(("%s_q%d_force420_lookahead%d" % (name, q, la), os.path.join(d, "input.rgb"),
+                          int(meta["w"]), int(meta["h"]), q, {"force_420": 1, "lookahead": la}))
+        run_e2e(manifest, cases, section="e2e_420")
     if "e2e-edge" in what:
         # the reference's edge paths (processor.cc):
         #  - images under 32 px in either dimension: no comparator, the q=1
