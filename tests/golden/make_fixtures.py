@@ -158,6 +158,13 @@ def main():
             ("tex_100x77_q95_oldmodel", tex, 100, 77, 95, {"new_model": 0}),
             ("tex_100x77_q95_lookahead2", tex, 100, 77, 95, {"lookahead": 2}),
         ], section="e2e_params")
+    if "e2e-params-la" in what:
+        # lookahead above 3 (the 4:4:4 search evaluates a step's candidates in
+        # batches of three: 4 is a full batch and a short one, 7 three batches)
+        tex = os.path.join(HERE, "stages_tex_100x77", "input.rgb")
+        run_e2e(manifest, [("tex_100x77_q95_lookahead4", tex, 100, 77, 95, {"lookahead": 4}),
+                           ("tex_100x77_q90_lookahead7", tex, 100, 77, 90, {"lookahead": 7})],
+                section="e2e_params")
     if "e2e-420" in what:
         # the 4:2:0 pass (Params::try_420 / force_420 / use_silver_screen,
         # processor.cc:986-1016): downsampled search alone, both passes, the
