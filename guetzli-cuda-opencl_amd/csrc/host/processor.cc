@@ -3150,6 +3150,15 @@ int Processor::Run420(const JpegData& jpg_in, std::string* err) {
   };
   if (!cmp_->SetOriginalCoeffs420(jpg420)) return device_error();
   Image420 img;
+  // (a candidate's bytes may still be in the writer thread, which reads
+  // img's saved JpegData: joined before img goes out of scope on every
+  // return -- the normal one applies its MaybeOutput first, below)
+  struct JoinWriter {
+    std::thread* t;
+    ~JoinWriter() {
+      if (t->joinable()) t->join();
+    }
+  } join_writer{&writer_};
   img.Init(jpg420.width, jpg420.height);
   // SelectQuantMatrix (processor.cc:340-372) with the downsampling generator
   int best_q[3][kDCTBlockSize];
@@ -3181,6 +3190,7 @@ int Processor::Run420(const JpegData& jpg_in, std::string* err) {
   res_->seconds_quantize += Since(tq);
   if (!SelectFrequencyMasking420(jpg420, &img, 1, 0.97f, false, err)) return GZ_ERR_DEVICE;
   if (!SelectFrequencyMasking420(jpg420, &img, 6, 1.0, true, err)) return GZ_ERR_DEVICE;
+  FlushOutput();  // (the last candidate's MaybeOutput, with its own Compare's distance)
   return GZ_OK;
 }
 
