@@ -3307,6 +3307,7 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
   AcBlockModel acm;
   size_t acm_base[3];
   acm.Build(*img, acm_base);
+  size_t chroma_updates = 0;
   res_->seconds_backend += Since(tb0);
   bool first_up_iter = true;
   for (int direction : {1, -1}) {
@@ -3364,7 +3365,8 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
         coeff_t* block = img->block(c, bix);
         acm.ChangeAt<JpegHistogram, false>(acm_base[c] + bix, c, block, k, static_cast<coeff_t>(newval), quant,
                                            nullptr, &ac_histograms[c], nullptr);
-        img->SetCoeffBlock(c, bix, block);  // (the chroma's pixel update)
+        img->SetCoeffBlock(c, bix, block);  // (the chroma's pixel update: 0.5 us, 0.17 s of a 1080p force_420)
+        chroma_updates += c != 0;
         last_indexes[bix] += direction;
         loop.Applied(global_order[i].second);
         if (loop.CodesRead(i)) ac_histogram_size = static_cast<int>(ComputeEntropyCodes(ac_histograms, &ac_depths));
@@ -3377,6 +3379,8 @@ bool Processor::SelectFrequencyMasking420(const JpegData& jpg, Image420* img, in
       ++res_->iterations;
       if (direction > 0) ++res_->iterations_up; else ++res_->iterations_down;
       res_->detail["backend420_changes"] += loop.changed;
+      res_->detail["backend420_chroma_updates"] += static_cast<double>(chroma_updates);
+      chroma_updates = 0;
       res_->seconds_backend += Since(tb);
       BeginOutput420(jpg, img);
       const auto tc = Clock::now();
