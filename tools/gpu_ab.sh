@@ -6,7 +6,7 @@
 #   bash tools/gpu_ab.sh VARIANT ...
 #
 # VARIANT = name[:spec[,spec...]], spec one of
-#   lib=PATH    an alternative libguetzli_hip.so (GZ_LIB_PATH; built under _ab/)
+#   lib=PATH    an alternative libguetzli_hip.so (GZ_LIB_PATH; tools/build_variant.sh builds one under _abv/)
 #   tree=DIR    bench.py, Python binding and library of another tree (e.g. a
 #               previous round's checkout copied under _ab/)
 #   K=V         an environment setting (GZ_SPIN_US=0, GPU_MAX_HW_QUEUES=8 ...)
