@@ -305,6 +305,11 @@ def dist_setup(n_gpus, backend=None):
     if world > 1:
         import torch
         import torch.distributed as dist
+        if os.environ.get("GZ_BENCH_ONE_DEVICE") == "1":
+            # (rehearsal of the N-rank flow on a one-GPU box: every rank on
+            # device 0, collectives over gloo on host tensors)
+            local = 0
+            backend = "gloo"
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
@@ -677,6 +682,8 @@ def main():
 
     dev = local
     torch.cuda.set_device(dev)
+    # (collective tensors: on the device for RCCL, on the host for gloo)
+    cdev = "cpu" if dist is not None and dist.get_backend() == "gloo" else "cuda:%d" % dev
     w, h, q = args.width, args.height, args.quality
     params = gz.Params.for_quality(q)
     nsteps = args.warmup + args.steps
@@ -711,7 +718,7 @@ def main():
         out = [r[0] for r in res]
         if dist is not None:
             # the final gather of the JPEG byte strings over RCCL/xGMI
-            gathered = sharding.gather_bytes(out, dist, "cuda:%d" % dev)
+            gathered = sharding.gather_bytes(out, dist, cdev)
             assert gathered[rank] == out
         return out, [r[1] for r in res]
 
@@ -762,10 +769,10 @@ def main():
              if (hashlib.sha256(data).hexdigest(), it) == kn[sd])
     counts = [len(checked), ok]
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor(counts, dtype=torch.int64, device=f"cuda:{dev}")
+        c = torch.tensor(counts, dtype=torch.int64, device=cdev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         counts = [int(v) for v in c.tolist()]
 
@@ -782,78 +789,103 @@ def main():
         host[k] = getattr(st1, k)
     host.update(gz.last_process_detail())
 
+    out = None
+    if rank == 0:
+        total_px = world * args.steps * args.frames_per_step * w * h
+        value = total_px / elapsed / 1e6
+
+        rep = frame_report(prof, w, h, int(host.get("candidates", 0)))
+        regions = rep["regions"]
+        uhd = None if args.no_uhd_frame else uhd_frame(gz, dev)
+        gpu_frame_ms = sum(ms for ms, _, _ in regions)
+
+        out = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": "%d synthetic %dx%d sRGB frames per GPU per step, %d encoding "
+                                   "at once, q=%d, guetzli::Process end to end (%s)" % (
+                                       args.frames_per_step, w, h, in_flight, q, frame_config(w, h, q)),
+                       "width": w, "height": h, "quality": q,
+                       "frames_per_gpu_per_step": args.frames_per_step,
+                       "frames_in_flight": in_flight,
+                       "host_pool_threads": int(os.environ.get("GZ_HOST_THREADS", "0")) or "library default",
+                       "schedule": "lockstep steps" if args.lockstep else
+                                   "one queue over the timed steps' frames",
+                       "parallelism": "image-sharded over %d GPU(s)%s" % (
+                           world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
+                       "search_iterations": iters},
+            "verified": {"frames": counts[0], "bit_exact": counts[1],
+                         "against": "reference guetzli --c sha256 + iterations "
+                                    "(tests/golden/manifest.json)"},
+            "roofline": north_star_roofline(uhd) or rep["dominant"],
+            "zeroing_roofline": rep["dominant"],
+            "compare_roofline": rep["compare_roofline"],
+            "compare_pass": rep["compare_pass"],
+            "blur_mask_pass": rep["blur_mask_pass"],
+            "stages": rep["stages"],
+            "gpu_ms_per_frame_isolated": round(gpu_frame_ms, 3),
+            "gpu_regions_ms_per_frame": {n: round(ms, 4) for ms, n, _ in regions},
+            "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
+            "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
+            "host_cores_busy_per_gpu": round(cpu_s / elapsed, 2),
+            "host_cpu_user_system_seconds_per_frame": [
+                round((ru1.ru_utime - ru0.ru_utime) / (args.steps * args.frames_per_step), 4),
+                round((ru1.ru_stime - ru0.ru_stime) / (args.steps * args.frames_per_step), 4)],
+            "single_frame": {"seconds": round(single_s, 4),
+                             "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
+                             "iterations": st1.iterations,
+                             "host_breakdown_seconds": {k: round(v, 4) for k, v in host.items()}},
+        }
+        if uhd is not None:
+            out["configs2_4k"] = uhd
+            out["blur_mask_pass_4k"] = uhd["blur_mask_pass"]
     large = None
     if not args.no_large_frame:
         # (a side leg after the timed region: a failure there is reported in
-        # the line instead of losing it)
+        # the line instead of losing it; with N >= 4 its strip ranks exchange
+        # through collectives, and a watchdog prints the line without the leg
+        # and ends every rank if the leg has not finished in
+        # GZ_STRIP_LEG_LIMIT seconds)
+        watchdog = None
+        if world >= 4:
+            import threading
+            leg_done = threading.Event()
+            limit = float(os.environ.get("GZ_STRIP_LEG_LIMIT", "240"))
+
+            def watch():
+                if leg_done.wait(limit):
+                    return
+                if rank == 0:
+                    out["configs4_8192"] = {"config": "BASELINE configs[4]",
+                                            "error": "strip leg unfinished after %.0f s" % limit}
+                    print(json.dumps(out), flush=True)
+                print("configs[4] leg unfinished after %.0f s on rank %d: exiting" % (limit, rank),
+                      file=sys.stderr, flush=True)
+                os._exit(3 if counts[1] != counts[0] else 0)
+            watchdog = threading.Thread(target=watch, daemon=True)
+            watchdog.start()
         try:
             large = large_frame(gz, dist, world, rank, dev)
         except Exception as e:  # noqa: BLE001
             large = {"config": "BASELINE configs[4]", "error": repr(e)[:400]}
             print("configs[4] leg failed on rank %d: %r" % (rank, e), file=sys.stderr, flush=True)
+        if watchdog is not None:
+            leg_done.set()
     if rank != 0:
         pool.shutdown()
         if dist is not None:
             dist.destroy_process_group()
         return
-    total_px = world * args.steps * args.frames_per_step * w * h
-    value = total_px / elapsed / 1e6
-
-    rep = frame_report(prof, w, h, int(host.get("candidates", 0)))
-    regions = rep["regions"]
-    uhd = None if args.no_uhd_frame else uhd_frame(gz, dev)
-    gpu_frame_ms = sum(ms for ms, _, _ in regions)
-
-    out = {
-        "metric": METRIC,
-        "value": round(value, 4),
-        "unit": "Mpixels/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic",
-        "config": {"workload": "%d synthetic %dx%d sRGB frames per GPU per step, %d encoding "
-                               "at once, q=%d, guetzli::Process end to end (%s)" % (
-                                   args.frames_per_step, w, h, in_flight, q, frame_config(w, h, q)),
-                   "width": w, "height": h, "quality": q,
-                   "frames_per_gpu_per_step": args.frames_per_step,
-                   "frames_in_flight": in_flight,
-                   "host_pool_threads": int(os.environ.get("GZ_HOST_THREADS", "0")) or "library default",
-                   "schedule": "lockstep steps" if args.lockstep else
-                               "one queue over the timed steps' frames",
-                   "parallelism": "image-sharded over %d GPU(s)%s" % (
-                       world, ", RCCL all_gather of JPEG bytes" if world > 1 else ""),
-                   "search_iterations": iters},
-        "verified": {"frames": counts[0], "bit_exact": counts[1],
-                     "against": "reference guetzli --c sha256 + iterations "
-                                "(tests/golden/manifest.json)"},
-        "roofline": north_star_roofline(uhd) or rep["dominant"],
-        "zeroing_roofline": rep["dominant"],
-        "compare_roofline": rep["compare_roofline"],
-        "compare_pass": rep["compare_pass"],
-        "blur_mask_pass": rep["blur_mask_pass"],
-        "stages": rep["stages"],
-        "gpu_ms_per_frame_isolated": round(gpu_frame_ms, 3),
-        "gpu_regions_ms_per_frame": {n: round(ms, 4) for ms, n, _ in regions},
-        "concurrent_frame_breakdown_seconds": {k: round(v, 4) for k, v in conc.items()},
-        "host_cpu_seconds_per_frame": round(cpu_per_frame, 4),
-        "host_cores_busy_per_gpu": round(cpu_s / elapsed, 2),
-        "host_cpu_user_system_seconds_per_frame": [
-            round((ru1.ru_utime - ru0.ru_utime) / (args.steps * args.frames_per_step), 4),
-            round((ru1.ru_stime - ru0.ru_stime) / (args.steps * args.frames_per_step), 4)],
-        "single_frame": {"seconds": round(single_s, 4),
-                         "Mpixels_per_s": round(w * h / single_s / 1e6, 4),
-                         "iterations": st1.iterations,
-                         "host_breakdown_seconds": {k: round(v, 4) for k, v in host.items()}},
-    }
-    if uhd is not None:
-        out["configs2_4k"] = uhd
-        out["blur_mask_pass_4k"] = uhd["blur_mask_pass"]
     if large is not None:
         out["configs4_8192"] = large
     if not args.no_cpu_baseline and world == 1:
