@@ -1479,7 +1479,7 @@ bool Engine::OrderBuild(int direction, int rblock, double target_distance, bool 
   g.blo = ord_lo_;
   g.bhi = std::min(ord_hi_, nb_);
   ord_h1_summed_ = false;
-  if (direction < 0)
+  if (direction < 0 && (rblock > 1 || !GZ_FUSE_ACTIVE))  // (radius 1: formed by the build itself)
     GZ_TIMED("order_build", k_order_active<<<static_cast<unsigned>((nb_ + 255) / 256), 256, 0, s>>>(
                                 d_block_max_, zero_bmax ? 1 : 0, bw_, bh_, rblock, target_distance,
                                 reinterpret_cast<int*>(base + L.active)));
@@ -1528,7 +1528,7 @@ bool Engine::OrderFetch(std::pair<int, float>* out, size_t n) {
     if (cnt == 0) continue;
     if (cnt < 0 || base < 0 || static_cast<size_t>(base) + cnt > n || at + cnt > n)
       return Fail("OrderFetch: workgroup ranges", 0);
-    memcpy(out + at, src + base, static_cast<size_t>(cnt) * sizeof(OrderEntry));
+    memcpy(static_cast<void*>(out + at), src + base, static_cast<size_t>(cnt) * sizeof(OrderEntry));
     at += static_cast<size_t>(cnt);
   }
   if (at != n) return Fail("OrderFetch: entry count", 0);
