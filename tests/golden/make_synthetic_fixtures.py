@@ -39,6 +39,12 @@ CASES = {
     "synth_1920x1080_s0_q90": (0, 1920, 1080, 90),
     "gray_1920x1080_s0_q95": (0, 1920, 1080, 95, "gray"),
     "gray_640x360_s3_q90": (3, 640, 360, 90, "gray"),
+    # round 6: configs[2]'s size at the headline quality, and sizes off the
+    # 16-pixel grid (partial blocks and MCUs) at other qualities
+    "synth_3840x2160_s1_q95": (1, 3840, 2160, 95),
+    "synth_2560x1440_s2_q92": (2, 2560, 1440, 92),
+    "synth_1366x768_s5_q88": (5, 1366, 768, 88),
+    "synth_1283x721_s4_q84": (4, 1283, 721, 84),
 }
 
 
