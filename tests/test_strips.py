@@ -213,6 +213,8 @@ def _gpu_strip_rank(rank, world, port, e, q, force=False):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,world,force", [("bees_q95", 1, True), ("bees_q95", 1, False), ("bees_q90", 2, False),
+                                              ("synth_1366x768_s5_q88", 3, False),
+                                              ("synth_2560x1440_s2_q92", 4, False),
                                               ("synth_8192x8192_s0_q84", 4, False)])
 def test_gpu_strips_reproduce_reference(name, world, force):
     """`world` ranks, each a process with its strip's engine on cuda:0, the
