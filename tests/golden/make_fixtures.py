@@ -251,6 +251,16 @@ def main():
         run_e2e(manifest, [("synth_1920x1080_s0_q95_force420", rgb, 1920, 1080, 95, {"force_420": 1})],
                 section="e2e_420")
         manifest["e2e_420"]["synth_1920x1080_s0_q95_force420"]["input"] = "synthetic:0"
+    if "e2e-420-synth" in what:
+        # the 4:2:0 pass on a frame off the 16-pixel grid (partial chroma
+        # blocks on both edges): synthetic 1366x768 seed 5, q90, force_420
+        sys.path.insert(0, os.path.join(ROOT, "guetzli-cuda-opencl_amd", "python"))
+        import guetzli_amd as gz
+        rgb = "/tmp/gz_fixture_synth_1366x768_s5.rgb"
+        gz.synthetic_frame(5, 1366, 768).tofile(rgb)
+        run_e2e(manifest, [("synth_1366x768_s5_q90_force420", rgb, 1366, 768, 90, {"force_420": 1})],
+                section="e2e_420")
+        manifest["e2e_420"]["synth_1366x768_s5_q90_force420"]["input"] = "synthetic:5"
     json.dump(manifest, open(manifest_path, "w"), indent=1, sort_keys=True)
 
 
