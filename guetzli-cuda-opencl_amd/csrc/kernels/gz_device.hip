@@ -847,7 +847,7 @@ bool Engine::EnqueueCompare(CompareDebug* dbg) {
     const int rows = env_rows > 0 ? env_rows : OpsinStreamRows(w_, h_);
     const int strips = (w_ + kOsCols - 1) / kOsCols, segs = (h_ + rows - 1) / rows;
     float* xyb_dbg = dbg && dbg->cand_xyb ? d_xyb_ : nullptr;
-    GZ_TIMED("opsin_mhic", k_opsin_mhic_stream<<<(strips * segs + 3) / 4, 256, 0, s>>>(
+    GZ_TIMED("opsin_mhic", (GZ_OS_PAIR ? k_opsin_mhic_stream2 : k_opsin_mhic_stream)<<<(strips * segs + 3) / 4, 256, 0, s>>>(
         d_px8_, d_ref_xyb_, w_, h_, strips, segs, rows, d_m0_, d_m1_, xyb_dbg, d_scales_,
         scale_stride_, d_dmax_));
     if (xyb_dbg && !d2h(dbg->cand_xyb, d_xyb_, 3 * n)) return false;

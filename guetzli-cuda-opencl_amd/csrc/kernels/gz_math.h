@@ -401,6 +401,105 @@ __device__ __forceinline__ void mhic_mix(const float c0[3], const float c1[3], c
 }
 
 // ---------------------------------------------------------------------------
+// Two pixels at once (f32x2: v_pk_* instructions, two IEEE operations each):
+// every function below applies to each half exactly the operation sequence
+// of its scalar form above, so each half's value is bit-identical to the
+// scalar result for that pixel.  (Packed f32 halves the issue slots of the
+// VALU-bound streams: round 6, profiles/round6_opsin_pair_ab.txt.)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x2 splat2(float v) { return f32x2{v, v}; }
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 sel2(bool kx, bool ky, f32x2 a, f32x2 b) {
+  return f32x2{kx ? a.x : b.x, ky ? a.y : b.y};
+}
+
+__device__ __forceinline__ void opsin_absorbance2(f32x2 r, f32x2 g, f32x2 b, f32x2 out[3]) {
+  out[0] = splat2(0.348036746003f) * r + splat2(0.577814843137f) * g + splat2(0.0544556093735f) * b +
+           splat2(0.774145581713f);
+  out[1] = splat2(0.26922717275f) * r + splat2(0.767247733938f) * g + splat2(0.0366922708552f) * b +
+           splat2(0.920130265014f);
+  out[2] = splat2(0.0882062883536f) * r + splat2(0.158581714673f) * g + splat2(0.712857943858f) * b +
+           splat2(10.6524069248f);
+}
+
+// fdiv_normal per half (the reciprocal per half, the corrections packed)
+__device__ __forceinline__ f32x2 fdiv_normal2(f32x2 a, f32x2 b) {
+  f32x2 y = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  const f32x2 e = fma2(-b, y, splat2(1.0f));
+  y = fma2(e, y, y);
+  f32x2 q = a * y;
+  f32x2 r = fma2(-b, q, a);
+  q = fma2(r, y, q);
+  r = fma2(-b, q, a);
+  return fma2(r, y, q);
+}
+
+__device__ __forceinline__ f32x2 fdiv_gamma_range2(f32x2 n) {
+  constexpr float d = 274.579999999999984f - 0.770000000000000f;
+  constexpr float r = 1.0f / d;
+  const f32x2 q = n * splat2(r);
+  const f32x2 e = fma2(-q, splat2(d), n);
+  return fma2(e, splat2(r), q);
+}
+
+// clenshaw6x2's recursion for one polynomial at two points
+__device__ __forceinline__ f32x2 clenshaw6_at2(f32x2 xx, float c0, float c1, float c2, float c3, float c4,
+                                               float c5) {
+  f32x2 b1 = splat2(c5), b2 = {0.0f, 0.0f}, xb, t;
+  xb = xx * b1; t = (xb + xb) - b2 + splat2(c4); b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + splat2(c3); b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + splat2(c2); b2 = b1; b1 = t;
+  xb = xx * b1; t = (xb + xb) - b2 + splat2(c1); b2 = b1; b1 = t;
+  xb = xx * b1;
+  return xb - b2 + splat2(c0);
+}
+
+__device__ __forceinline__ f32x2 gamma_poly2(f32x2 x) {
+  const f32x2 x01 = fdiv_gamma_range2(x - splat2(0.770000000000000f));
+  const f32x2 xc = splat2(2.0f) * x01 - splat2(1.0f);
+  const f32x2 yp = clenshaw6_at2(xc, 881.979476556478289f, 1496.058452015812463f, 908.662212739659481f,
+                                 373.566100223287378f, 85.840860336314364f, 6.683258861509244f);
+  const f32x2 yq = clenshaw6_at2(xc, 12.262350348616792f, 20.557285797683576f, 12.161463238367844f,
+                                 4.711532733641639f, 0.899112889751053f, 0.035662329617191f);
+  const f32x2 g = fdiv_normal2(yp, yq);
+  return sel2(yq.x == 0.0f, yq.y == 0.0f, splat2(0.0f), g);
+}
+
+__device__ __forceinline__ void opsin_pixel2(const f32x2 blurred[3], const f32x2 lin[3], f32x2 xyb[3]) {
+  f32x2 pm[3], sens[3], cm[3];
+  opsin_absorbance2(blurred[0], blurred[1], blurred[2], pm);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) sens[c] = fdiv_normal2(gamma_poly2(pm[c]), pm[c]);
+  opsin_absorbance2(lin[0], lin[1], lin[2], cm);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) cm[c] *= sens[c];
+  xyb[0] = splat2(1.01611726948f) * cm[0] - splat2(0.982482243696f) * cm[1];
+  xyb[1] = splat2(1.43571362627f) * cm[0] + splat2(0.896039849412f) * cm[1];
+  xyb[2] = cm[2];
+}
+
+__device__ __forceinline__ f32x2 mhic_ave2(f32x2 a, f32x2 b) { return (a + b) * splat2(0.5f); }
+__device__ __forceinline__ f32x2 mhic_sqdiff2(f32x2 n0, f32x2 n1, f32x2 ave_y) {
+  const f32x2 d = (n0 + n1) * splat2(0.5f) - ave_y;
+  return d * d;
+}
+__device__ __forceinline__ void mhic_mix2(const f32x2 c0[3], const f32x2 c1[3], const f32x2 ave[3],
+                                          f32x2 sqr_max_diff, f32x2 x0[3], f32x2 x1[3]) {
+  const float kRX = 275.19165240059317f, kRY = 18599.41286306991f;
+  const float kRZ = 410.8995306951065f, kChroma = 106.95800948271017f;
+  const f32x2 chroma_scale = fdiv_normal2(splat2(kChroma), ave[1] + splat2(kChroma));
+  const f32x2 mix[3] = {fdiv_normal2(chroma_scale * splat2(kRX), sqr_max_diff + splat2(kRX)),
+                        fdiv_normal2(splat2(kRY), sqr_max_diff + splat2(kRY)),
+                        fdiv_normal2(chroma_scale * splat2(kRZ), sqr_max_diff + splat2(kRZ))};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    x0[c] = mix[c] * c0[c] + (splat2(1.0f) - mix[c]) * ave[c];
+    x1[c] = mix[c] * c1[c] + (splat2(1.0f) - mix[c]) * ave[c];
+  }
+}
+
+
+// ---------------------------------------------------------------------------
 // Colour conversion (color_transform.h:211-218) and sRGB -> linear
 // ---------------------------------------------------------------------------
 
