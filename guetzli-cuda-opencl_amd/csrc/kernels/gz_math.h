@@ -191,6 +191,38 @@ __device__ __forceinline__ float interp_f(const float* a, int size, float sx) {
   return sx < 0 ? -res : res;
 }
 
+// interp_f over a paired table t[i] = (a[i], a[i + 1] - a[i]) for i < size - 1
+// and t[size - 1] = (a[size - 1], 0): one 8-byte read, no branch.  The same
+// operations on the same values: the difference is the same f32 subtraction,
+// mix = ix - trunc(ix) is exact (v_fract; for ix >= 2^23 both are 0), and an
+// index at or past size - 1 takes a[size - 1] + mix * 0 == a[size - 1] (mix is
+// finite and >= 0, so the product is +0).
+__device__ __forceinline__ float interp_pair_f(const float2* t, int size, float sx) {
+  const float ix = fabsf(sx);
+  const int base = static_cast<int>(ix);
+  const float mix = __builtin_amdgcn_fractf(ix);
+  const float2 p = t[base < size - 1 ? base : size - 1];
+  const float res = p.x + mix * p.y;
+  return sx < 0 ? -res : res;
+}
+
+// sqrtf of x >= 0 (finite) where x == 0 or x >= 2^-96: the hardware square
+// root (within 1 ulp) corrected by the signs of its two neighbours' residuals
+// -- the compiler's own correctly rounded sequence without its scaling of
+// inputs below 2^-96 and its class test (x == 0: the lower neighbour is a NaN,
+// the upper one's residual +0, so 0 stays).  sqrt_needs_scale() flags the
+// inputs it does not cover; a wave with any takes sqrtf.
+__device__ __forceinline__ float sqrt_cr_big(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float dn = __uint_as_float(__float_as_uint(s) - 1u);
+  const float up = __uint_as_float(__float_as_uint(s) + 1u);
+  const float r = fmaf(-dn, s, x) <= 0.0f ? dn : s;
+  return fmaf(-up, s, x) > 0.0f ? up : r;
+}
+__device__ __forceinline__ bool sqrt_needs_scale(float x) {  // 0 < x < 2^-96
+  return __float_as_uint(x) - 1u < 0x0f7fffffu;
+}
+
 __device__ __forceinline__ float interp_clamp_neg_f(const float* a, int size, float sx) {
   // InterpolateClampNegativeOpt, :212-229
   if (sx < 0) sx = 0;
@@ -228,18 +260,26 @@ __device__ __forceinline__ void lowfreq_sq_zero_f(float x, float y, float z, flo
   res[2] += factor * vz * vz;
 }
 
-// (lf_dy: c_tab.lf_dy or an LDS copy of it)
+// interp_f over lf_dy as a plain table or as interp_pair_f's paired one
+__device__ __forceinline__ float interp_tab(const float* a, int size, float sx) { return interp_f(a, size, sx); }
+__device__ __forceinline__ float interp_tab(const float2* t, int size, float sx) {
+  return interp_pair_f(t, size, sx);
+}
+
+// (lf_dy: c_tab.lf_dy or an LDS copy of it, plain or paired)
+template <class Tab = float>
 __device__ __forceinline__ void lowfreq_vals_f(float x, float y, float z, float v[3],
-                                               const float* lf_dy = c_tab.lf_dy) {
+                                               const Tab* lf_dy = c_tab.lf_dy) {
   z += 0.0812519812628f * y;
   v[2] = z * 7.34905756986f;
   v[0] = x * 6.64482198135f;
-  v[1] = interp_f(lf_dy, 21, y * 0.837846224276f);
+  v[1] = interp_tab(lf_dy, 21, y * 0.837846224276f);
 }
 
 // General two-colour form (used by the corner edge detector).
+template <class Tab = float>
 __device__ __forceinline__ void lowfreq_sq_f(const float a[3], const float b[3], float factor,
-                                             float res[3], const float* lf_dy = c_tab.lf_dy) {
+                                             float res[3], const Tab* lf_dy = c_tab.lf_dy) {
   float v0[3];
   lowfreq_vals_f(a[0], a[1], a[2], v0, lf_dy);
   if (b[0] == 0.0f && b[1] == 0.0f && b[2] == 0.0f) {
