@@ -130,6 +130,10 @@ void BuildTables(GzTables* t) {
   for (int i = 0; i < 37; ++i) {
     t->block_csf[i] = static_cast<float>(kBlockCsfD[i]);
     t->block_csf_d[i] = kBlockCsfD[i];
+    // k_block_diff2's X / B term csf[k] * 64.8f * v is (csf[k] * 64.8f) * v:
+    // its first product, the same f32 multiply
+    t->csf_xb[0][i] = t->block_csf[i] * 64.8f;
+    t->csf_xb[1][i] = t->block_csf[i] * 2.4f;
   }
   // the AC sums' term csf_d[k] * 64.8 * sq[k] is (csf_d[k] * 64.8) * sq[k]:
   // its first product per k, formed here with the same double multiply

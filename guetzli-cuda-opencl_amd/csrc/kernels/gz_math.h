@@ -90,6 +90,7 @@ struct GzTables {
   float block_csf[37];                             // :103-144
   double block_csf_d[37];                          // butteraugli.cc:157-198
   double ac_w_d[3][33];  // block_csf_d[k] * 64.8, 1.0, block_csf_d[k] * 2.4 (k = 4..36): the AC sums' factors
+  float csf_xb[2][37];   // block_csf[k] * 64.8f, block_csf[k] * 2.4f: the X / B terms' first product (f32)
   float zeroing_csf[192];                          // order.inc:3
   uint8_t zigzag[64];                              // kJPEGZigZagOrder, jpeg_data.h:73-82
   uint8_t old_csf[64];                             // oldCsf, processor.cc:381-390

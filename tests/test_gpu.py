@@ -682,3 +682,38 @@ def test_compare_stages_at_frame_size(gz, name):
     assert np.float32(cmp.compare(cand)) == np.float32(e["distance"])
     dm = cmp.distmap()
     assert hashlib.sha256(np.ascontiguousarray(dm, np.float32).tobytes()).hexdigest() == e["sha256"]["distmap"]
+
+
+def _interp_tables():
+    """hf_dy / lf_dy as the library's table setup forms them (gz_device.hip,
+    f32 running sums)."""
+    hf = np.zeros(21, np.float32)
+    lf = np.zeros(21, np.float32)
+    hf[1] = np.float32(1.4103373714040413)
+    for i in range(2, 21):
+        hf[i] = hf[i - 1] + np.float32(0.7084088867024)
+    for i in range(1, 21):
+        lf[i] = lf[i - 1] + np.float32(5.2511644570349185)
+    return hf, lf
+
+
+@pytest.mark.parametrize("which", ["sqrt", "interp_hf", "interp_lf", "interp_random"])
+def test_block_diff_sqrt_and_interp_exhaustive(which):
+    """k_block_diff2's replacements, exhaustively on the device: bd_sqrt's
+    pre-scaled hardware root + residual correction equals the compiler's
+    correctly rounded sqrtf for every float in [0, 2^96) (the Y operands are
+    |F|^2 * 0.000064 of bounded planes, far below 2^96), and interp_pair_f
+    over the paired table equals interp_f (InterpolateOpt,
+    clbutter_comparator.cpp:195-210) for every finite argument, on both
+    tables the kernel uses and a random one (tests/native/sqrt_check.hip)."""
+    import ctypes
+    here = os.path.dirname(os.path.abspath(__file__))
+    lib = ctypes.CDLL(os.path.join(here, "_build", "libgz_helper_check.so"))
+    hf, lf = _interp_tables()
+    tab = {"sqrt": hf, "interp_hf": hf, "interp_lf": lf,
+           "interp_random": np.sort(np.random.default_rng(5).random(21, np.float32) * 40)}[which]
+    tab = np.ascontiguousarray(tab, np.float32)
+    out = (ctypes.c_ulonglong * 2)()
+    rc = lib.gz_helper_check(0 if which == "sqrt" else 1, tab.ctypes.data_as(ctypes.c_void_p), out)
+    assert rc == 0
+    assert out[0] == 0, "%d mismatches, first bit pattern %#010x" % (out[0], out[1])
