@@ -326,16 +326,30 @@ __device__ __forceinline__ void opsin_absorbance(float r, float g, float b, floa
   out[2] = 0.0882062883536f * r + 0.158581714673f * g + 0.712857943858f * b + 10.6524069248f;
 }
 
+#ifndef GZ_CLENSHAW_2X
+#define GZ_CLENSHAW_2X 1
+#endif
 __device__ __forceinline__ f32x2 clenshaw6x2(float x, f32x2 c0, f32x2 c1, f32x2 c2, f32x2 c3,
                                              f32x2 c4, f32x2 c5) {
   const f32x2 xx = {x, x};
   // the first step from b1 = b2 = 0 gives exactly c5 for finite x
   // ((x * 0 + x * 0) - 0 is a zero, and a zero plus c5 != 0 is c5)
   f32x2 b1 = c5, b2 = {0.0f, 0.0f}, xb, t;
+#if GZ_CLENSHAW_2X
+  // xb + xb of the reference's step as (2 x) * b1: doubling is exact and
+  // commutes with the product's rounding (nothing here comes near the
+  // subnormal range or overflow), one operation fewer per step
+  const f32x2 x2 = xx + xx;
+  xb = x2 * b1; t = xb - b2 + c4; b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + c3; b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + c2; b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + c1; b2 = b1; b1 = t;
+#else
   xb = xx * b1; t = (xb + xb) - b2 + c4; b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + c3; b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + c2; b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + c1; b2 = b1; b1 = t;
+#endif
   xb = xx * b1;
   return xb - b2 + c0;
 }
@@ -487,10 +501,18 @@ __device__ __forceinline__ f32x2 fdiv_gamma_range2(f32x2 n) {
 __device__ __forceinline__ f32x2 clenshaw6_at2(f32x2 xx, float c0, float c1, float c2, float c3, float c4,
                                                float c5) {
   f32x2 b1 = splat2(c5), b2 = {0.0f, 0.0f}, xb, t;
+#if GZ_CLENSHAW_2X
+  const f32x2 x2 = xx + xx;  // (clenshaw6x2's doubling)
+  xb = x2 * b1; t = xb - b2 + splat2(c4); b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + splat2(c3); b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + splat2(c2); b2 = b1; b1 = t;
+  xb = x2 * b1; t = xb - b2 + splat2(c1); b2 = b1; b1 = t;
+#else
   xb = xx * b1; t = (xb + xb) - b2 + splat2(c4); b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + splat2(c3); b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + splat2(c2); b2 = b1; b1 = t;
   xb = xx * b1; t = (xb + xb) - b2 + splat2(c1); b2 = b1; b1 = t;
+#endif
   xb = xx * b1;
   return xb - b2 + splat2(c0);
 }
