@@ -2,7 +2,7 @@
 // k_block_diff2 against the forms they replace (tests/test_gpu.py::
 // test_block_diff_sqrt_and_interp_exhaustive).
 //
-//  * bd_sqrt's square root -- the hardware root corrected by its neighbours'
+//  * k_block_diff2's square root -- the hardware root corrected by its neighbours'
 //    residuals, on inputs pre-scaled by 2^32 -- against the compiler's
 //    correctly rounded sqrtf, bit for bit, for every float in [0, 2^96).
 //  * interp_pair_f over a paired table against interp_f over the plain table
@@ -19,7 +19,7 @@ namespace {
 
 constexpr unsigned kSqrtEnd = (127u + 96u) << 23;  // bit pattern of 2^96
 
-__device__ __forceinline__ float sqrt_scaled(float x) {  // bd_sqrt with GZ_BD_SQRT_GUARD 2
+__device__ __forceinline__ float sqrt_scaled(float x) {  // (the kernel keeps the result scaled by 2^16)
   return gz::sqrt_cr_big(x * 0x1p32f) * 0x1p-16f;
 }
 

@@ -699,8 +699,9 @@ def _interp_tables():
 
 @pytest.mark.parametrize("which", ["sqrt", "interp_hf", "interp_lf", "interp_random"])
 def test_block_diff_sqrt_and_interp_exhaustive(which):
-    """k_block_diff2's replacements, exhaustively on the device: bd_sqrt's
-    pre-scaled hardware root + residual correction equals the compiler's
+    """k_block_diff2's replacements, exhaustively on the device: its square root's
+    hardware root + residual correction on 2^32-scaled inputs (sqrt_cr_big;
+    the kernel carries the result scaled by 2^16) equals, scaled back, the compiler's
     correctly rounded sqrtf for every float in [0, 2^96) (the Y operands are
     |F|^2 * 0.000064 of bounded planes, far below 2^96), and interp_pair_f
     over the paired table equals interp_f (InterpolateOpt,
